@@ -1,0 +1,62 @@
+"""Build libcustma_hip.so for gfx950 with hipcc (in-tree, so it travels with
+the repo snapshot to the GPU box).  Usage: python -m custereomatching_amd.build
+
+Each .hip translation unit is compiled separately (parallel) and linked
+into one shared library exporting the C ABI of include/custma.h.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "_lib")
+LIB = os.path.join(LIBDIR, "libcustma_hip.so")
+SOURCES = ["capi.hip", "stats.hip", "fwd_exact.hip", "sweep_fwd.hip", "sweep_bwd.hip", "select.hip"]
+ARCH = os.environ.get("CUSTMA_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -ffp-contract=off: fused multiply-adds only where written (__builtin_fmaf / fma);
+# the exact path replays the reference's nvcc contraction explicitly.
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
+          "-fno-gpu-rdc", "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+
+
+def _obj(src):
+    return os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
+
+
+def _deps():
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip"))] + [
+        os.path.join(HERE, "..", "include", "custma.h")]
+
+
+def _compile(src):
+    out = _obj(src)
+    cmd = [HIPCC, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return out
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    newest = max(os.path.getmtime(p) for p in _deps())
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
+        return LIB
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,187 @@
+// C ABI of libcustma_hip.so (declared in include/custma.h).
+// Validation, workspace carving and dispatch; no allocation, no
+// synchronisation (graph-capturable).  Error behaviour: every entry point
+// returns a CUSTMA_E_* code and records a message for custma_last_error(),
+// which the Python shim raises as RuntimeError / ValueError -- unlike the
+// reference, which checks only device/contiguity (custma/include/
+// stereo_matching.hpp:20-33), asserts the shape in debug builds only
+// (custma/src/stereo_matching.cpp:28) and never checks its launches
+// (custma/src/stereo_matching_kernel.cu:203,237,252).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+#include "sweep.h"
+
+namespace custma {
+size_t backward_transpose_bytes(const Geo& g);
+
+namespace {
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_hip(hipError_t e, const char* what) {
+    if (e == hipSuccess) return CUSTMA_OK;
+    return fail(CUSTMA_E_LAUNCH, "%s: HIP error %d (%s)", what, (int)e, hipGetErrorString(e));
+}
+
+size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+int make_geo(int64_t H, int64_t W, int32_t k, int32_t layout, int32_t D, Geo* g) {
+    if (H < 0 || W < 0) return fail(CUSTMA_E_ARG, "image size must be non-negative, got H=%lld W=%lld",
+                                    (long long)H, (long long)W);
+    if (k < 1 || (k & 1) == 0 || k > CUSTMA_MAX_KERNEL)
+        return fail(CUSTMA_E_ARG, "kernel_size must be odd and in [1, %d], got %d", CUSTMA_MAX_KERNEL, k);
+    if (layout != CUSTMA_LAYOUT_FULL && layout != CUSTMA_LAYOUT_WINDOW)
+        return fail(CUSTMA_E_ARG, "unknown layout %d", layout);
+    if (layout == CUSTMA_LAYOUT_WINDOW && (D < 0 || (int64_t)D >= W))
+        return fail(CUSTMA_E_ARG, "window layout needs 0 <= D < W, got D=%d W=%lld", D, (long long)W);
+    g->H = H; g->W = W; g->k = k; g->r = k / 2; g->layout = layout;
+    g->D = layout == CUSTMA_LAYOUT_WINDOW ? D : 0;
+    g->WO = layout == CUSTMA_LAYOUT_WINDOW ? W - D : W;
+    g->DO = layout == CUSTMA_LAYOUT_WINDOW ? (int64_t)D + 1 : W;
+    return CUSTMA_OK;
+}
+
+size_t stats_bytes(const Geo& g) { return 2 * align256((size_t)g.H * g.W * 20); }
+
+void carve_stats(const Geo& g, void* ws, Stats* sc, Stats* sp) {
+    const size_t n = (size_t)g.H * g.W;
+    char* p = (char*)ws;
+    Stats* s[2] = {sc, sp};
+    for (int i = 0; i < 2; ++i) {
+        char* base = p + i * align256(n * 20);
+        s[i]->box = (double*)base;
+        s[i]->mean = (float*)(base + n * 8);
+        s[i]->sq = s[i]->mean + n;
+        s[i]->sqt = s[i]->sq + n;
+    }
+}
+
+int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, void* ws, Stats* sc, Stats* sp,
+              hipStream_t s) {
+    carve_stats(g, ws, sc, sp);
+    int rc = check_hip(launch_stats(cam, dtype, g, *sc, s), "stats(camera)");
+    if (rc) return rc;
+    return check_hip(launch_stats(proj, dtype, g, *sp, s), "stats(projector)");
+}
+
+int check_dtype(int32_t dtype) {
+    if (dtype != CUSTMA_F32 && dtype != CUSTMA_F16)
+        return fail(CUSTMA_E_ARG, "unsupported dtype code %d (float32=0, float16=1)", dtype);
+    return CUSTMA_OK;
+}
+}  // namespace
+
+bool fast_supported(int k) {
+    switch (k) {
+#define CUSTMA_K(KK) case KK:
+        CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+        return true;
+        default: return false;
+    }
+}
+
+}  // namespace custma
+
+using namespace custma;
+
+extern "C" {
+
+int custma_abi_version(void) { return 1; }
+
+const char* custma_last_error(void) { return g_err; }
+
+int custma_volume_dims(int64_t H, int64_t W, int32_t layout, int32_t D, int64_t* wo, int64_t* dout) {
+    Geo g;
+    int rc = make_geo(H, W, 1, layout, D, &g);
+    if (rc) return rc;
+    if (wo) *wo = g.WO;
+    if (dout) *dout = g.DO;
+    return CUSTMA_OK;
+}
+
+size_t custma_workspace_bytes(int64_t H, int64_t W, int32_t kernel_size, int32_t layout, int32_t D, int32_t op) {
+    Geo g;
+    if (make_geo(H, W, kernel_size, layout, D, &g)) return 0;
+    size_t n = stats_bytes(g);
+    if (op == CUSTMA_OP_DISPARITY) n += align256(disparity_partial_bytes(g));
+    if (op == CUSTMA_OP_BACKWARD) n += align256(backward_partial_bytes(g)) + align256(backward_transpose_bytes(g));
+    return n;
+}
+
+int custma_forward(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                   int32_t kernel_size, int32_t layout, int32_t D, int32_t precision, float* cost_volume,
+                   void* workspace, size_t workspace_bytes, void* stream) {
+    Geo g;
+    int rc = make_geo(H, W, kernel_size, layout, D, &g);
+    if (rc || (rc = check_dtype(dtype))) return rc;
+    if (precision != CUSTMA_EXACT && precision != CUSTMA_FAST)
+        return fail(CUSTMA_E_ARG, "unknown precision %d", precision);
+    if (g.H == 0 || g.W == 0) return CUSTMA_OK;
+    if (!camera || !projector || !cost_volume || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
+    if (workspace_bytes < stats_bytes(g)) return fail(CUSTMA_E_WORKSPACE, "workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    Stats sc, sp;
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
+    if (precision == CUSTMA_FAST && fast_supported(g.k))
+        return check_hip(launch_fwd_fast(camera, projector, dtype, g, sc, sp, cost_volume, s), "forward(fast)");
+    return check_hip(launch_fwd_exact(camera, projector, dtype, g, sc, sp, cost_volume, s), "forward(exact)");
+}
+
+int custma_backward(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
+                    int64_t W, int32_t kernel_size, int32_t layout, int32_t D, float* camera_grad,
+                    float* projector_grad, void* workspace, size_t workspace_bytes, void* stream) {
+    Geo g;
+    int rc = make_geo(H, W, kernel_size, layout, D, &g);
+    if (rc || (rc = check_dtype(dtype))) return rc;
+    if (!fast_supported(g.k))
+        return fail(CUSTMA_E_UNSUPPORTED, "backward supports odd kernel_size <= 15, got %d", g.k);
+    if (g.H == 0 || g.W == 0 || (!camera_grad && !projector_grad)) return CUSTMA_OK;
+    if (!grad || !camera || !projector || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
+    const size_t need = stats_bytes(g) + align256(backward_partial_bytes(g)) +
+                        (projector_grad ? align256(backward_transpose_bytes(g)) : 0);
+    if (workspace_bytes < need) return fail(CUSTMA_E_WORKSPACE, "workspace too small (%zu < %zu)", workspace_bytes, need);
+    hipStream_t s = (hipStream_t)stream;
+    Stats sc, sp;
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
+    void* ws2 = (char*)workspace + stats_bytes(g);
+    return check_hip(launch_backward(grad, camera, projector, dtype, g, sc, sp, camera_grad, projector_grad, ws2, s),
+                     "backward");
+}
+
+int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, float* best, void* stream) {
+    if (rows < 0 || n < 0) return fail(CUSTMA_E_ARG, "negative size");
+    if (rows == 0) return CUSTMA_OK;
+    if (n == 0) return fail(CUSTMA_E_ARG, "argmax over an empty axis");
+    if (!volume || !index) return fail(CUSTMA_E_NULL, "null pointer argument");
+    return check_hip(launch_argmax(volume, rows, n, index, best, (hipStream_t)stream), "argmax");
+}
+
+int custma_disparity(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                     int32_t kernel_size, int32_t layout, int32_t D, int64_t* index, float* best,
+                     int32_t* n_rechecked, void* workspace, size_t workspace_bytes, void* stream) {
+    Geo g;
+    int rc = make_geo(H, W, kernel_size, layout, D, &g);
+    if (rc || (rc = check_dtype(dtype))) return rc;
+    if (g.H == 0 || g.W == 0) return CUSTMA_OK;
+    if (!camera || !projector || !index || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
+    if (workspace_bytes < stats_bytes(g) + align256(disparity_partial_bytes(g)))
+        return fail(CUSTMA_E_WORKSPACE, "workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    Stats sc, sp;
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
+    void* ws2 = (char*)workspace + stats_bytes(g);
+    return check_hip(launch_disparity(camera, projector, dtype, g, sc, sp, index, best, n_rechecked, ws2, s),
+                     "disparity");
+}
+
+}  // extern "C"

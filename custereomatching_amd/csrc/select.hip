@@ -1,0 +1,203 @@
+// Disparity selection.
+//
+//  * k_argmax: first-index argmax over the volume's last axis -- what the
+//    reference's callers do with torch.max / torch.argmax on the returned
+//    volume (examples/verify.py:72, examples/test.py:78-83).
+//  * fused, certified disparity (no volume): the fast sweep writes per
+//    disparity-chunk (best, second, index) partials; k_disp_merge combines
+//    them and CERTIFIES a pixel when its top-2 gap exceeds twice the fast
+//    path's error bound (then the fast argmax is provably the exact argmax);
+//    every other pixel is queued and k_disp_recheck re-decides it with the
+//    reference arithmetic (exact k*k fma chain, stereo_matching_kernel.cu:39-71).
+//    The reported best cost is always recomputed exactly.  So the index map is
+//    bit-identical to argmax of the exact volume.
+#include <float.h>
+
+#include "common.h"
+#include "sweep.h"
+
+namespace custma {
+
+namespace {
+
+// torch.argmax semantics: NaN is the maximum, first index on ties.
+// Start from (-inf, INT64_MAX) so the first element always wins.
+__device__ __forceinline__ void amax_merge(float& bv, int64_t& bi, float ov, int64_t oi) {
+    bool take;
+    if (bv != bv) take = (ov != ov) && oi < bi;
+    else if (ov != ov) take = true;
+    else take = ov > bv || (ov == bv && oi < bi);
+    if (take) { bv = ov; bi = oi; }
+}
+
+__global__ __launch_bounds__(256) void k_argmax(const float* __restrict__ vol, int64_t rows, int64_t n,
+                                                int64_t* __restrict__ idx, float* __restrict__ best) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t row = wave; row < rows; row += nwaves) {
+        const float* v = vol + row * n;
+        float bv = -INFINITY;
+        int64_t bi = INT64_MAX;
+        for (int64_t s = lane; s < n; s += 64) {
+            amax_merge(bv, bi, v[s], s);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ov = __shfl_xor(bv, off);
+            const int64_t oi = __shfl_xor(bi, off);
+            amax_merge(bv, bi, ov, oi);
+        }
+        if (lane == 0) {
+            idx[row] = bi;
+            if (best) best[row] = bv;
+        }
+    }
+}
+
+// Exact reference cost of one voxel (stereo_matching_kernel.cu:39-71, nvcc
+// -fmad=true), using the stats pass's bit-identical means and moments.
+template <typename T>
+__device__ float exact_cost(const T* cam, const T* proj, const Geo& g, const Stats& sc, const Stats& sp, int64_t h,
+                            int64_t w, int64_t d) {
+    const float mc = sc.mean[h * g.W + w], mp = sp.mean[h * g.W + d];
+    float e = 0.f;
+    for (int i = 0; i < g.k; ++i)
+        for (int j = 0; j < g.k; ++j) {
+            const float c = ldpad(cam, g.H, g.W, h + i - g.r, w + j - g.r) - mc;
+            const float p = ldpad(proj, g.H, g.W, h + i - g.r, d + j - g.r) - mp;
+            e = __builtin_fmaf(c, p, e);
+        }
+    const float den = sqrtf(__builtin_fmaf(sc.sq[h * g.W + w], sp.sq[h * g.W + d], kEps));
+    return (e + kEps) / den;
+}
+
+__device__ __forceinline__ int64_t d_of_s(const Geo& g, int64_t w, int64_t s) {
+    return g.layout == CUSTMA_LAYOUT_WINDOW ? w + s : s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
+                                                    Stats sc, Stats sp, DispPartial part, int nChunk, float tau,
+                                                    int64_t* __restrict__ idx, float* __restrict__ best,
+                                                    int32_t* __restrict__ counter, int64_t* __restrict__ queue) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t npix = g.H * g.WO;
+    if (p >= npix) return;
+    float b = -FLT_MAX, sec = -FLT_MAX;
+    int64_t bi = INT64_MAX;
+    for (int c = 0; c < nChunk; ++c) {
+        const int64_t q = (int64_t)c * npix + p;
+        const int32_t oi = part.index[q];
+        if (oi < 0) continue;
+        const float ob = part.best[q], os = part.second[q];
+        if (ob > b || (ob == b && oi < bi)) {
+            sec = fmaxf(os, b); b = ob; bi = oi;
+        } else {
+            sec = fmaxf(sec, ob);
+        }
+    }
+    const int64_t h = p / g.WO, w = p % g.WO;
+    if (bi != INT64_MAX && (sec == -FLT_MAX || b - sec > tau)) {
+        idx[p] = bi;
+        if (best) best[p] = exact_cost(cam, proj, g, sc, sp, h, w, d_of_s(g, w, bi));
+    } else {
+        const int32_t slot = atomicAdd(counter, 1);
+        queue[slot] = p;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_disp_recheck(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
+                                                      Stats sc, Stats sp, const int32_t* __restrict__ counter,
+                                                      const int64_t* __restrict__ queue, int64_t* __restrict__ idx,
+                                                      float* __restrict__ best) {
+    __shared__ float rv[4];
+    __shared__ int64_t ri[4];
+    const int n = *counter;
+    for (int64_t e = blockIdx.x; e < n; e += gridDim.x) {
+        const int64_t p = queue[e];
+        const int64_t h = p / g.WO, w = p % g.WO;
+        float bv = -INFINITY;
+        int64_t bi = INT64_MAX;
+        for (int64_t s = threadIdx.x; s < g.DO; s += blockDim.x) {
+            const int64_t d = d_of_s(g, w, s);
+            if (!voxel_valid(g, w, d)) continue;
+            const float c = exact_cost(cam, proj, g, sc, sp, h, w, d);
+            amax_merge(bv, bi, c, s);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ov = __shfl_xor(bv, off);
+            const int64_t oi = __shfl_xor(bi, off);
+            amax_merge(bv, bi, ov, oi);
+        }
+        const int wave = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) { rv[wave] = bv; ri[wave] = bi; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int q = 1; q < (int)(blockDim.x >> 6); ++q) amax_merge(bv, bi, rv[q], ri[q]);
+            idx[p] = bi;
+            if (best) best[p] = bv;
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+hipError_t launch_argmax(const float* vol, int64_t rows, int64_t n, int64_t* idx, float* best, hipStream_t s) {
+    const int64_t waves = rows < 2048 * 4 ? rows : 2048 * 4;
+    const int64_t blocks = cdiv(waves, 4);
+    hipLaunchKernelGGL(k_argmax, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0, s, vol, rows, n, idx, best);
+    return hipGetLastError();
+}
+
+size_t disparity_partial_bytes(const Geo& g) {
+    const SweepGrid sg = sweep_grid(g);
+    const size_t n = (size_t)sg.nChunk * g.H * g.WO;
+    return n * (4 + 4 + 4) + (size_t)g.H * g.WO * 8 + 256;
+}
+
+hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
+                            int64_t* idx, float* best, int32_t* n_rechecked, void* ws, hipStream_t s) {
+    const SweepGrid sg = sweep_grid(g);
+    const size_t n = (size_t)sg.nChunk * g.H * g.WO;
+    char* p = (char*)ws;
+    int32_t* counter = (int32_t*)p;  // 256 B header
+    p += 256;
+    int64_t* queue = (int64_t*)p;
+    p += (size_t)g.H * g.WO * 8;
+    DispPartial part;
+    part.best = (float*)p;
+    part.second = part.best + n;
+    part.index = (int32_t*)(part.second + n);
+    hipError_t e = hipMemsetAsync(counter, 0, 4, s);
+    if (e != hipSuccess) return e;
+    // kernel sizes without a sweep instantiation: every pixel is decided exactly
+    const int nChunk = fast_supported(g.k) ? sg.nChunk : 0;
+    if (nChunk) {
+        e = launch_disp_partials(cam, proj, dtype, g, sc, sp, part, s);
+        if (e != hipSuccess) return e;
+    }
+    // certification margin: 2 x twice the fast path's worst-case error
+    const float tau = (float)(8.0 * (g.k * g.k + 6) * 5.9604644775390625e-08);
+    const int64_t npix = g.H * g.WO;
+    const unsigned mb = (unsigned)cdiv(npix, 256);
+    if (dtype == CUSTMA_F16) {
+        hipLaunchKernelGGL(k_disp_merge<__half>, dim3(mb), dim3(256), 0, s, (const __half*)cam, (const __half*)proj,
+                           g, sc, sp, part, nChunk, tau, idx, best, counter, queue);
+        hipLaunchKernelGGL(k_disp_recheck<__half>, dim3(2048), dim3(256), 0, s, (const __half*)cam,
+                           (const __half*)proj, g, sc, sp, counter, queue, idx, best);
+    } else {
+        hipLaunchKernelGGL(k_disp_merge<float>, dim3(mb), dim3(256), 0, s, (const float*)cam, (const float*)proj, g,
+                           sc, sp, part, nChunk, tau, idx, best, counter, queue);
+        hipLaunchKernelGGL(k_disp_recheck<float>, dim3(2048), dim3(256), 0, s, (const float*)cam,
+                           (const float*)proj, g, sc, sp, counter, queue, idx, best);
+    }
+    e = hipGetLastError();
+    if (e == hipSuccess && n_rechecked) e = hipMemcpyAsync(n_rechecked, counter, 4, hipMemcpyDeviceToDevice, s);
+    return e;
+}
+
+}  // namespace custma

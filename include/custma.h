@@ -1,0 +1,101 @@
+/*
+ * custma.h -- C ABI of the MI355X (gfx950) ZNCC stereo cost-volume library
+ * (libcustma_hip.so).  Plain pointers, sizes and a hipStream_t passed as
+ * void*; no torch types.  Every entry point returns 0 on success or a
+ * negative CUSTMA_E_* code; custma_last_error() returns the message of the
+ * last failure on the calling thread.
+ *
+ * Each entry point replaces a piece of the reference extension
+ * (lzhnb/CuStereoMatching @ v0), cited file:line below.  Device pointers
+ * must be on the current HIP device; images are row-major [H, W],
+ * contiguous, of element type `dtype`.  Outputs are written fully (no
+ * pre-zeroing needed).  `workspace` is device memory of at least
+ * custma_workspace_bytes(...) bytes, owned by the caller (the torch caching
+ * allocator in the Python shim); nothing is allocated inside a call, so
+ * every call is hipGraph-capturable.
+ */
+#ifndef CUSTMA_H
+#define CUSTMA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element type of the images */
+#define CUSTMA_F32 0
+#define CUSTMA_F16 1
+
+/* volume layout */
+#define CUSTMA_LAYOUT_FULL 0   /* [H, W, W]: out[h][w][d], every projector column d (reference behaviour,
+                                  custma/src/stereo_matching_kernel.cu:35-37, :200) */
+#define CUSTMA_LAYOUT_WINDOW 1 /* [H, W-D, D+1]: out[h][w][s] = full[h][w][w+s] (the reference's
+                                  commented-out intent, stereo_matching_kernel.cu:30-33, :192-198) */
+
+/* forward arithmetic */
+#define CUSTMA_EXACT 0 /* bit-identical to the reference arithmetic (nvcc -fmad=true): per voxel a k*k-long
+                          fp32 fma chain, IEEE sqrt and divide (stereo_matching_kernel.cu:39-71) */
+#define CUSTMA_FAST 1  /* fp64 sliding-window sums: |cost - exact| <= (k^2+6) 2^-24 */
+
+/* ops for custma_workspace_bytes */
+#define CUSTMA_OP_FORWARD 0
+#define CUSTMA_OP_BACKWARD 1
+#define CUSTMA_OP_DISPARITY 2
+
+/* error codes */
+#define CUSTMA_OK 0
+#define CUSTMA_E_ARG (-1)       /* bad scalar argument (shape, kernel size, layout, D, dtype) */
+#define CUSTMA_E_NULL (-2)      /* null pointer where one is required */
+#define CUSTMA_E_WORKSPACE (-3) /* workspace too small */
+#define CUSTMA_E_LAUNCH (-4)    /* HIP launch / runtime error */
+#define CUSTMA_E_UNSUPPORTED (-5)
+
+#define CUSTMA_MAX_KERNEL 31
+
+int custma_abi_version(void);
+const char* custma_last_error(void);
+
+/* Volume dims for a layout: *wo = W (full) or W-D (window); *dout = W or D+1. */
+int custma_volume_dims(int64_t H, int64_t W, int32_t layout, int32_t D, int64_t* wo, int64_t* dout);
+
+size_t custma_workspace_bytes(int64_t H, int64_t W, int32_t kernel_size, int32_t layout, int32_t D,
+                              int32_t op);
+
+/* Forward cost volume.
+ * Replaces stereo::stereo_matching_forward (custma/src/stereo_matching.cpp:16-42) and
+ * stereo::stereo_matching_forward_wrapper + forward_cost_volume_kernel
+ * (custma/src/stereo_matching_kernel.cu:17-72, :182-216).
+ * `D` is ignored for CUSTMA_LAYOUT_FULL, exactly like the reference. */
+int custma_forward(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                   int32_t kernel_size, int32_t layout, int32_t D, int32_t precision, float* cost_volume,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* Backward: gradients of sum(grad * cost_volume) w.r.t. both images.
+ * Replaces stereo::stereo_matching_backward (custma/src/stereo_matching.cpp:45-73) and
+ * stereo_matching_backward_wrapper + get_patches_grad_kernel + patches_grad_to_image_kernel
+ * (custma/src/stereo_matching_kernel.cu:75-179, :218-261).  Deterministic (no atomics).
+ * camera_grad / projector_grad may each be NULL (not computed); the reference computes the
+ * camera gradient only (custma/stereo_matching_wrapper.py:33). */
+int custma_backward(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
+                    int64_t W, int32_t kernel_size, int32_t layout, int32_t D, float* camera_grad,
+                    float* projector_grad, void* workspace, size_t workspace_bytes, void* stream);
+
+/* First-index argmax over the last axis of a [rows, n] fp32 array (torch.argmax semantics), as the
+ * reference's callers do on the volume (examples/verify.py:72, examples/test.py:78-83). */
+int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, float* best, void* stream);
+
+/* Fused disparity without materialising the volume: index[h][w] = argmax_s cost(h, w, s) (first index
+ * on ties; s as in the layout), best[h][w] = that cost.  Computed by the fast path and certified: every
+ * pixel whose fast top-2 gap is below the fast path's error margin is re-decided with the exact
+ * reference arithmetic, so `index` is bit-identical to argmax of the CUSTMA_EXACT volume.
+ * n_rechecked (device int32, may be NULL) receives the number of re-decided pixels. */
+int custma_disparity(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                     int32_t kernel_size, int32_t layout, int32_t D, int64_t* index, float* best,
+                     int32_t* n_rechecked, void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CUSTMA_H */

@@ -1,0 +1,95 @@
+"""PyTorch CPU restatement of the reference's torch path -- TEST INFRASTRUCTURE ONLY.
+
+Restates examples/verify.py:18-28 (``extract_image_patch_pytoch``: zero pad,
+unfold columns then rows, [H, W, k, k] patches) and :81-133
+(``torch_cost_volume_backward``: centre, EXY = bmm, EX2/EY2, cost =
+(EXY + eps) / sqrt(EX2 * EY2 + eps), autograd backward).  This is "the repo's
+Python/CPU fallback" that bench.py times as ``cpu_baseline`` (kind "port").
+
+``row_chunk`` processes output rows in bands with a k//2 halo; rows are
+independent (output row h reads input rows h-r..h+r only), so the arithmetic
+per voxel is unchanged and memory stays bounded at large sizes.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+EPS = 1e-8  # examples/verify.py:112
+
+
+def patches(img: torch.Tensor, k: int) -> torch.Tensor:
+    """[H, W] -> [H, W, k*k] zero-padded patches, tap order (i, j) row-major."""
+    r = k // 2
+    x = F.pad(img[None, None], (r, r, r, r), mode="constant", value=0.0)
+    x = x.unfold(3, k, 1).unfold(2, k, 1).permute(0, 1, 2, 3, 5, 4)  # [1,1,H,W,k,k]
+    H, W = img.shape
+    return x.reshape(H, W, k * k)
+
+
+def cost_volume(cam: torch.Tensor, proj: torch.Tensor, k: int) -> torch.Tensor:
+    """Full [H, W, W] ZNCC volume, differentiable (verify.py:107-120)."""
+    pc = patches(cam, k)
+    pp = patches(proj, k)
+    pc = pc - pc.mean(dim=-1, keepdim=True)
+    pp = pp - pp.mean(dim=-1, keepdim=True)
+    exy = torch.bmm(pc, pp.transpose(1, 2))
+    ex2 = (pc * pc).sum(-1, keepdim=True)
+    ey2 = (pp * pp).sum(-1).unsqueeze(-2)
+    return (exy + EPS) / torch.sqrt(ex2 * ey2 + EPS)
+
+
+def forward_backward(cam, proj, k, grad=None, proj_grad=True, row_chunk=None):
+    """Returns (volume, camera_grad, projector_grad) on CPU.
+
+    grad=None means ones (verify.py:123).  With row_chunk the volume is not
+    returned (None) and gradients are accumulated band by band.
+    """
+    H, W = cam.shape
+    r = k // 2
+    if row_chunk is None or row_chunk >= H:
+        c = cam.detach().clone().requires_grad_(True)
+        p = proj.detach().clone().requires_grad_(proj_grad)
+        v = cost_volume(c, p, k)
+        v.backward(torch.ones_like(v) if grad is None else grad)
+        return v.detach(), c.grad, (p.grad if proj_grad else None)
+    gc = torch.zeros_like(cam)
+    gp = torch.zeros_like(proj)
+    for h0 in range(0, H, row_chunk):
+        h1 = min(H, h0 + row_chunk)
+        a0, a1 = max(0, h0 - r), min(H, h1 + r)
+        c = cam[a0:a1].detach().clone().requires_grad_(True)
+        p = proj[a0:a1].detach().clone().requires_grad_(proj_grad)
+        # The band's own zero padding differs from the image's at interior
+        # band edges, so compute on the haloed band and keep rows h0..h1.
+        v = band_volume(c, p, k, h0 - a0, h1 - a0, top_pad=(a0 == 0), bot_pad=(a1 == H))
+        g = torch.ones_like(v) if grad is None else grad[h0:h1]
+        v.backward(g)
+        gc[a0:a1] += c.grad
+        if proj_grad:
+            gp[a0:a1] += p.grad
+    return None, gc, (gp if proj_grad else None)
+
+
+def band_volume(c, p, k, o0, o1, top_pad, bot_pad):
+    """Volume rows o0..o1 of a haloed band.  Rows outside the band that exist
+    in the full image are present in c/p as halo, so only true image borders
+    are zero padded (F.pad on the band pads halo edges too, but those padded
+    rows only feed output rows outside o0..o1)."""
+    v = cost_volume(c, p, k)
+    return v[o0:o1]
+
+
+def forward_only(cam, proj, k, row_chunk=None):
+    """Forward volume without autograd (for CPU forward timing)."""
+    with torch.no_grad():
+        if row_chunk is None or row_chunk >= cam.shape[0]:
+            return cost_volume(cam, proj, k)
+        H = cam.shape[0]
+        r = k // 2
+        outs = []
+        for h0 in range(0, H, row_chunk):
+            h1 = min(H, h0 + row_chunk)
+            a0, a1 = max(0, h0 - r), min(H, h1 + r)
+            outs.append(cost_volume(cam[a0:a1], proj[a0:a1], k)[h0 - a0:h1 - a0])
+        return torch.cat(outs)

@@ -1,0 +1,124 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+entry point include/custma.h declares, validates arguments before touching
+the device, and the Python shim raises the reference's error messages."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "custma.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(custma_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from custereomatching_amd import _lib
+
+    syms = declared_symbols()
+    assert len(syms) >= 8
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (custma_\w+)", out))
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    for s in syms:
+        assert hasattr(_lib.lib, s)
+    assert set(_lib.EXPORTS) <= set(syms)
+
+
+def test_library_is_gfx950_code_object():
+    from custereomatching_amd import _lib
+
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob  # offload bundle entry for gfx950
+
+
+def test_abi_version_and_dims():
+    from custereomatching_amd import _lib
+
+    assert _lib.lib.custma_abi_version() == 1
+    assert _lib.volume_dims(128, 256, _lib.LAYOUT_FULL, 0) == (256, 256)
+    assert _lib.volume_dims(128, 256, _lib.LAYOUT_WINDOW, 32) == (224, 33)
+    with pytest.raises(ValueError):
+        _lib.volume_dims(128, 256, _lib.LAYOUT_WINDOW, 256)
+    assert _lib.workspace_bytes(64, 64, 5, 0, 0, _lib.OP_FORWARD) > 0
+    assert _lib.workspace_bytes(64, 64, 4, 0, 0, _lib.OP_FORWARD) == 0  # even kernel rejected
+
+
+@pytest.mark.parametrize("k", [0, 2, 33, -1])
+def test_forward_rejects_bad_kernel_without_device(k):
+    from custereomatching_amd import _lib
+
+    rc = _lib.lib.custma_forward(None, None, 0, 8, 8, k, 0, 0, 1, None, None, 0, None)
+    assert rc == _lib.E_ARG
+    assert b"kernel_size" in _lib.lib.custma_last_error()
+
+
+def test_entry_points_validate_before_launch():
+    from custereomatching_amd import _lib
+
+    L = _lib.lib
+    assert L.custma_forward(None, None, 7, 8, 8, 5, 0, 0, 1, None, None, 0, None) == _lib.E_ARG  # dtype
+    assert L.custma_forward(None, None, 0, 8, 8, 5, 3, 0, 1, None, None, 0, None) == _lib.E_ARG  # layout
+    assert L.custma_forward(None, None, 0, 8, 8, 5, 1, 8, 1, None, None, 0, None) == _lib.E_ARG  # D >= W
+    assert L.custma_forward(None, None, 0, 8, 8, 5, 0, 0, 1, None, None, 0, None) == _lib.E_NULL
+    assert L.custma_forward(None, None, 0, 0, 8, 5, 0, 0, 1, None, None, 0, None) == 0  # empty image: no-op
+    assert L.custma_backward(None, None, None, 0, 8, 8, 17, 0, 0, None, None, None, 0, None) == _lib.E_UNSUPPORTED
+    assert L.custma_argmax(None, 4, 0, None, None, None) == _lib.E_ARG
+    assert L.custma_disparity(None, None, 0, 8, 8, 5, 0, 0, None, None, None, None, 0, None) == _lib.E_NULL
+
+
+def test_python_shim_reference_error_messages():
+    import custma
+
+    cam = torch.rand(8, 16)
+    proj = torch.rand(8, 16)
+    with pytest.raises(RuntimeError, match="camera must be a CUDA tensor"):
+        custma.stereo_matching(cam, proj, 4, 5)
+    with pytest.raises(RuntimeError, match="camera must be a CUDA tensor"):
+        custma.src.stereo_matching_forward(cam, proj, 4, 5)
+    with pytest.raises(RuntimeError, match="cost_volume_grad must be a CUDA tensor"):
+        custma.src.stereo_matching_backward(torch.zeros(8, 16, 16), cam, proj, 5)
+
+
+def test_drop_in_surface():
+    import custma
+
+    assert custma.__version__ == "0.0.1"
+    assert callable(custma.stereo_matching)
+    from custma.stereo_matching_wrapper import _StereoMatching, stereo_matching  # noqa: F401
+    from custma.src import stereo_matching_backward, stereo_matching_forward  # noqa: F401
+
+    t = custma.Timer(print_tmpl="x {:.2f}")
+    assert t.is_running and t.since_start() >= 0 and t.since_last_check() >= 0
+
+
+def test_product_never_imports_oracle():
+    """The oracle is test infrastructure only (task contract ③)."""
+    for pkg in ("custereomatching_amd", "custma"):
+        for dp, _, files in os.walk(os.path.join(ROOT, pkg)):
+            for f in files:
+                if f.endswith((".py", ".hip", ".h", ".cpp")):
+                    txt = open(os.path.join(dp, f)).read()
+                    assert not re.search(r"^\s*(from|import)\s+oracle", txt, re.M), f
+                    assert "liborc" not in txt and "zncc_oracle" not in txt, f
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+    """No CPU fallback: loading without the .so raises ImportError."""
+    import importlib.util
+
+    from custereomatching_amd import _lib
+
+    spec = importlib.util.spec_from_file_location("custma_lib_probe", _lib.__file__)
+    mod = importlib.util.module_from_spec(spec)
+    monkeypatch.setattr(os.path, "exists", lambda p: False if p.endswith("libcustma_hip.so") else True)
+    with pytest.raises(ImportError, match="no CPU fallback|There is no CPU fallback"):
+        spec.loader.exec_module(mod)

@@ -1,0 +1,280 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bars (task contract / BASELINE north_star):
+  * exact forward: bit-identical to the oracle's reference arithmetic
+    (nvcc -fmad=true flavour of stereo_matching_kernel.cu:39-71);
+  * fast forward: |cost - exact| <= (k^2+6) 2^-24 (oracle.cost_error_bound);
+  * disparity (fused, certified) and volume argmax: bit-identical indices;
+  * gradients (both images): |g - g_f64| <= 1e-5 * max(1, max|g_f64|).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.golden.inputs import make_pair
+
+import custereomatching_amd as cm
+
+pytestmark = pytest.mark.gpu
+
+FULL, WIN = "full", "window"
+
+
+def _dev(x, dev, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev).to(dtype)
+
+
+def _layout_args(layout, D):
+    return (O.FULL, 0) if layout == FULL else (O.WINDOW, D)
+
+
+def gpu_forward(cam, proj, k, layout, D, precision, dev, dtype=torch.float32):
+    out = cm.cost_volume_forward(_dev(cam, dev, dtype), _dev(proj, dev, dtype), D, k, layout, precision)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+CASES = [
+    # H, W, k, D, kind
+    (24, 48, 5, 16, "textured"),
+    (20, 48, 9, 16, "textured"),
+    (1, 32, 5, 8, "textured"),
+    (40, 12, 11, 4, "textured"),
+    (33, 70, 3, 20, "smooth"),
+    (17, 40, 1, 10, "textured"),
+    (30, 64, 15, 31, "quantized"),
+    (24, 48, 7, 0, "textured"),
+    (26, 40, 5, 39, "textured"),
+    (19, 37, 21, 9, "textured"),  # beyond the sweep instantiations: exact kernel only
+    (24, 48, 5, 16, "constant"),
+    (24, 48, 5, 16, "zeros"),
+]
+IDS = [f"{h}x{w}_k{k}_D{d}_{kind}" for h, w, k, d, kind in CASES]
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+@pytest.mark.parametrize("layout", [FULL, WIN])
+def test_exact_forward_bit_identical(gpu, case, layout):
+    H, W, k, D, kind = case
+    cam, proj = make_pair(H, W, max(D, 1), seed=11, kind=kind)
+    lay, Dl = _layout_args(layout, D)
+    ref = O.forward(cam, proj, k, layout=lay, D=Dl, contract=1)
+    got = gpu_forward(cam, proj, k, layout, D, "exact", gpu)
+    assert got.shape == ref.shape
+    mism = np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))
+    assert mism == 0, f"{mism}/{ref.size} voxels differ; max |d| {np.abs(got - ref).max()}"
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+@pytest.mark.parametrize("layout", [FULL, WIN])
+def test_fast_forward_within_bound(gpu, case, layout):
+    H, W, k, D, kind = case
+    cam, proj = make_pair(H, W, max(D, 1), seed=12, kind=kind)
+    lay, Dl = _layout_args(layout, D)
+    ref = O.forward(cam, proj, k, layout=lay, D=Dl, contract=1)
+    got = gpu_forward(cam, proj, k, layout, D, "fast", gpu)
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() <= O.cost_error_bound(k)
+    truth = O.forward_f64(cam, proj, k, layout=lay, D=Dl)
+    assert np.abs(got - truth).max() <= O.cost_error_bound(k)
+
+
+@pytest.mark.parametrize("precision", ["exact", "fast"])
+def test_fp16_inputs(gpu, precision):
+    H, W, k, D = 32, 64, 9, 20
+    cam, proj = make_pair(H, W, D, seed=5)
+    ch = cam.astype(np.float16).astype(np.float32)
+    ph = proj.astype(np.float16).astype(np.float32)
+    for layout in (FULL, WIN):
+        lay, Dl = _layout_args(layout, D)
+        ref = O.forward(ch, ph, k, layout=lay, D=Dl)
+        got = gpu_forward(cam, proj, k, layout, D, precision, gpu, dtype=torch.float16)
+        if precision == "exact":
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+        else:
+            assert np.abs(got - ref).max() <= O.cost_error_bound(k)
+
+
+def test_volume_argmax_bit_identical(gpu):
+    rng = np.random.default_rng(0)
+    vol = rng.integers(0, 7, size=(13, 29, 301)).astype(np.float32)  # many ties
+    vol[3, 4, :] = -np.inf
+    vol[5, 6, 17] = np.nan
+    idx, best = cm.volume_argmax(_dev(vol, gpu))
+    ridx = torch.from_numpy(vol).argmax(-1)
+    assert np.array_equal(idx.cpu().numpy(), ridx.numpy())
+    v2 = rng.standard_normal((7, 1000)).astype(np.float32)
+    i2, b2 = cm.volume_argmax(_dev(v2, gpu))
+    oi, ob = O.argmax(v2)
+    assert np.array_equal(i2.cpu().numpy(), oi) and np.array_equal(b2.cpu().numpy(), ob)
+
+
+DISP_CASES = [
+    (48, 96, 5, 24, "textured"),
+    (40, 80, 9, 30, "quantized"),
+    (30, 64, 11, 16, "smooth"),
+    (24, 48, 5, 16, "constant"),
+    (24, 48, 5, 16, "zeros"),
+    (20, 40, 17, 12, "textured"),  # no sweep instance: every pixel decided exactly
+]
+
+
+@pytest.mark.parametrize("case", DISP_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_{c[4]}" for c in DISP_CASES])
+@pytest.mark.parametrize("layout", [FULL, WIN])
+def test_disparity_certified_bit_identical(gpu, case, layout):
+    H, W, k, D, kind = case
+    cam, proj = make_pair(H, W, D, seed=21, kind=kind)
+    lay, Dl = _layout_args(layout, D)
+    ref = O.forward(cam, proj, k, layout=lay, D=Dl, contract=1)
+    ridx, rbest = O.argmax(ref)
+    idx, best, nre = cm.stereo_disparity(_dev(cam, gpu), _dev(proj, gpu), D, k, layout, return_rechecked=True)
+    idx, best = idx.cpu().numpy(), best.cpu().numpy()
+    assert np.array_equal(idx, ridx), f"{np.count_nonzero(idx != ridx)} pixels differ"
+    assert np.array_equal(best.view(np.uint32), rbest.view(np.uint32))
+    if kind in ("constant", "zeros"):
+        assert int(nre.item()) > 0  # ties everywhere: the exact re-decision ran
+
+
+def _rand_grad(shape, seed):
+    return np.random.default_rng(seed).standard_normal(shape).astype(np.float32)
+
+
+BWD_CASES = [
+    (16, 24, 5, 8, "textured"),
+    (24, 48, 9, 16, "textured"),
+    (20, 40, 7, 12, "smooth"),
+    (24, 48, 5, 16, "quantized"),
+    (1, 32, 5, 8, "textured"),
+    (40, 12, 11, 4, "textured"),
+    (22, 50, 15, 30, "textured"),
+    (24, 48, 3, 0, "textured"),
+    (24, 48, 5, 16, "constant"),
+]
+
+
+@pytest.mark.parametrize("case", BWD_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_D{c[3]}_{c[4]}" for c in BWD_CASES])
+@pytest.mark.parametrize("layout", [FULL, WIN])
+def test_backward_both_images(gpu, case, layout):
+    H, W, k, D, kind = case
+    cam, proj = make_pair(H, W, max(D, 1), seed=31, kind=kind)
+    lay, Dl = _layout_args(layout, D)
+    shape = O.volume_shape(H, W, lay, Dl)
+    g = _rand_grad(shape, 7)
+    rc, rp = O.backward_f64(g, cam, proj, k, layout=lay, D=Dl)
+    gc, gp = cm.cost_volume_backward(_dev(g, gpu), _dev(cam, gpu), _dev(proj, gpu), k, layout, D,
+                                     camera_grad=True, projector_grad=True)
+    gc, gp = gc.cpu().numpy(), gp.cpu().numpy()
+    tol_c = 1e-5 * max(1.0, np.abs(rc).max())
+    tol_p = 1e-5 * max(1.0, np.abs(rp).max())
+    assert np.abs(gc - rc).max() <= tol_c, np.abs(gc - rc).max() / max(1.0, np.abs(rc).max())
+    assert np.abs(gp - rp).max() <= tol_p, np.abs(gp - rp).max() / max(1.0, np.abs(rp).max())
+
+
+def test_backward_ones_matches_reference_golden(gpu):
+    """g = ones, exactly what examples/verify.py:68,123 backpropagates."""
+    import glob
+    import os
+
+    for p in sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*_k*.npz"))):
+        z = np.load(p)
+        if "vol32" not in z:
+            continue
+        cam, proj, k = z["cam"], z["proj"], int(z["k"])
+        H, W = cam.shape
+        g = torch.ones(H, W, W, device=gpu)
+        gc, gp = cm.cost_volume_backward(g, _dev(cam, gpu), _dev(proj, gpu), k, camera_grad=True,
+                                         projector_grad=True)
+        mc = max(1.0, np.abs(z["cg64"]).max())
+        mp = max(1.0, np.abs(z["pg64"]).max())
+        assert np.abs(gc.cpu().numpy() - z["cg64"]).max() <= 1e-5 * mc, p
+        assert np.abs(gp.cpu().numpy() - z["pg64"]).max() <= 1e-5 * mp, p
+
+
+def test_backward_deterministic(gpu):
+    cam, proj = make_pair(32, 64, 16, seed=2)
+    g = _dev(_rand_grad((32, 64, 64), 3), gpu)
+    a = cm.cost_volume_backward(g, _dev(cam, gpu), _dev(proj, gpu), 9, projector_grad=True)
+    b = cm.cost_volume_backward(g, _dev(cam, gpu), _dev(proj, gpu), 9, projector_grad=True)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_autograd_drop_in(gpu):
+    import custma
+
+    cam, proj = make_pair(20, 40, 10, seed=4)
+    c = _dev(cam, gpu).requires_grad_(True)
+    p = _dev(proj, gpu)
+    vol = custma.stereo_matching(c.contiguous(), p.contiguous(), 200, 5)  # verify.py:66 call shape
+    assert vol.shape == (20, 40, 40) and vol.requires_grad
+    vol.backward(torch.ones_like(vol))  # verify.py:68
+    rc, _ = O.backward_f64(np.ones((20, 40, 40), np.float32), cam, proj, 5)
+    assert np.abs(c.grad.cpu().numpy() - rc).max() <= 1e-5 * max(1, np.abs(rc).max())
+    assert p.grad is None
+    # superset: projector gradient on request, and .sum().backward() (stride-0 grad)
+    c2 = _dev(cam, gpu).requires_grad_(True)
+    p2 = _dev(proj, gpu).requires_grad_(True)
+    custma.stereo_matching(c2, p2, 0, 5).sum().backward()
+    _, rp = O.backward_f64(np.ones((20, 40, 40), np.float32), cam, proj, 5)
+    assert np.abs(p2.grad.cpu().numpy() - rp).max() <= 1e-5 * max(1, np.abs(rp).max())
+    # reference extension surface
+    v = custma.src.stereo_matching_forward(c.detach(), p, 0, 5)
+    gcam = custma.src.stereo_matching_backward(torch.ones_like(v), c.detach(), p, 5)
+    assert torch.allclose(gcam, c.grad, rtol=0, atol=1e-6 * float(c.grad.abs().max()))
+
+
+def test_errors_on_device(gpu):
+    c = torch.rand(8, 16, device=gpu)
+    with pytest.raises(RuntimeError, match="must be contiguous"):
+        cm.stereo_matching(c.t(), c.t(), 0, 5)
+    with pytest.raises(RuntimeError, match="expected scalar type Float but found Double"):
+        cm.stereo_matching(c.double(), c.double(), 0, 5)
+    with pytest.raises(ValueError, match="kernel_size"):
+        cm.stereo_matching(c, c, 0, 4)
+    with pytest.raises(ValueError):
+        cm.stereo_matching(c, c, 16, 5, layout="window")
+    e = torch.empty(0, 16, device=gpu)
+    assert cm.stereo_matching(e, e, 0, 5).shape == (0, 16, 16)
+
+
+# ---- larger sizes: property checks the oracle cannot afford whole ----
+
+def _band_oracle_forward(cam, proj, k, h0, h1, layout, D):
+    r = k // 2
+    a0, a1 = max(0, h0 - r), min(cam.shape[0], h1 + r)
+    lay, Dl = _layout_args(layout, D)
+    v = O.forward(cam[a0:a1], proj[a0:a1], k, layout=lay, D=Dl)
+    return v[h0 - a0:h1 - a0]
+
+
+@pytest.mark.parametrize("layout,D", [(FULL, 0), (WIN, 128)])
+def test_large_1024_rows_vs_oracle_bands(gpu, layout, D):
+    H, W, k = 1024, 1024, 9
+    cam, proj = make_pair(H, W, 128, seed=8)
+    c, p = _dev(cam, gpu), _dev(proj, gpu)
+    ex = cm.cost_volume_forward(c, p, D, k, layout, "exact")
+    fa = cm.cost_volume_forward(c, p, D, k, layout, "fast")
+    assert float((ex - fa).abs().max()) <= O.cost_error_bound(k)
+    for h0 in (0, 511, 1016):
+        ref = _band_oracle_forward(cam, proj, k, h0, h0 + 8, layout, D)
+        got = ex[h0:h0 + 8].cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    idx, best = cm.stereo_disparity(c, p, D, k, layout)
+    vi, vb = cm.volume_argmax(ex)
+    assert torch.equal(idx, vi)
+    assert torch.equal(best, vb)
+
+
+def test_large_backward_band_vs_oracle(gpu):
+    H, W, k = 256, 512, 9
+    r = k // 2
+    cam, proj = make_pair(H, W, 64, seed=9)
+    g = _rand_grad((H, W, W), 10)
+    gc, gp = cm.cost_volume_backward(_dev(g, gpu), _dev(cam, gpu), _dev(proj, gpu), k, projector_grad=True)
+    h0, h1 = 120, 126
+    a0, a1 = h0 - 2 * r, h1 + 2 * r
+    rc, rp = O.backward_f64(g[a0:a1], cam[a0:a1], proj[a0:a1], k)
+    rc, rp = rc[h0 - a0:h1 - a0], rp[h0 - a0:h1 - a0]
+    assert np.abs(gc[h0:h1].cpu().numpy() - rc).max() <= 1e-5 * max(1, np.abs(rc).max())
+    assert np.abs(gp[h0:h1].cpu().numpy() - rp).max() <= 1e-5 * max(1, np.abs(rp).max())

@@ -1,0 +1,126 @@
+"""Pin the CPU oracle (oracle/zncc_oracle.c) against the reference.
+
+Golden vectors (tests/golden/*.npz) were produced by the REFERENCE's own
+torch path, examples/verify.py:81-133, in fp32 and fp64
+(tests/golden/gen_golden.py).  The oracle restates the reference CUDA
+arithmetic (stereo_matching_kernel.cu:39-71, :97-179); these tests show it
+agrees with the reference's torch path to within the reference's own fp32
+rounding, and that the exact-arithmetic flavours are internally consistent.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+SMALL = sorted(p for p in glob.glob(os.path.join(GOLD, "*.npz")) if not os.path.basename(p).startswith("verify_"))
+VERIFY = sorted(glob.glob(os.path.join(GOLD, "verify_*.npz")))
+
+
+def _load(p):
+    z = np.load(p)
+    return z, z["cam"], z["proj"], int(z["k"]), int(z["D"])
+
+
+@pytest.mark.parametrize("path", SMALL, ids=os.path.basename)
+def test_literal_equals_hoisted(path):
+    """Per-voxel literal restatement == per-pixel-stats restatement, bitwise."""
+    _, cam, proj, k, D = _load(path)
+    for contract in (1, 0):
+        a = O.forward(cam, proj, k, contract=contract)
+        b = O.forward(cam, proj, k, contract=contract, literal=True)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("path", SMALL, ids=os.path.basename)
+def test_forward_vs_reference_golden(path):
+    z, cam, proj, k, D = _load(path)
+    v = O.forward(cam, proj, k)
+    bound = O.cost_error_bound(k)
+    # vs fp64 truth of the reference torch path (eps is 1e-8f here, 1e-8 there: ~1e-9 relative)
+    assert np.abs(v - z["vol64"]).max() <= bound
+    # vs the reference torch path in fp32 (both carry fp32 rounding)
+    assert np.abs(v - z["vol32"]).max() <= 2 * bound
+    # the oracle's own fp64 restatement reproduces the reference fp64 truth
+    assert np.abs(O.forward_f64(cam, proj, k) - z["vol64"]).max() < 1e-7
+
+
+@pytest.mark.parametrize("path", SMALL, ids=os.path.basename)
+def test_backward_vs_reference_golden(path):
+    z, cam, proj, k, D = _load(path)
+    H, W = cam.shape
+    g = np.ones((H, W, W), np.float32)
+    dc, dp = O.backward_f64(g, cam, proj, k)
+    mg = max(1.0, np.abs(z["cg64"]).max())
+    assert np.abs(dc - z["cg64"]).max() <= 1e-7 * mg
+    mp = max(1.0, np.abs(z["pg64"]).max())
+    assert np.abs(dp - z["pg64"]).max() <= 1e-7 * mp
+    # fp32 reference arithmetic (what the CUDA kernel computes, minus atomics)
+    fc, fp = O.backward(g, cam, proj, k)
+    assert np.abs(fc - z["cg64"]).max() <= 3e-5 * mg
+    assert np.abs(fp - z["pg64"]).max() <= 3e-5 * mp
+
+
+@pytest.mark.parametrize("path", VERIFY, ids=os.path.basename)
+def test_verify_config_golden(path):
+    """BASELINE configs[0]: 128x256, D=32, window 5."""
+    z, cam, proj, k, D = _load(path)
+    v = O.forward(cam, proj, k)
+    flat = v.reshape(-1)
+    bound = O.cost_error_bound(k)
+    assert np.abs(flat[z["sample_idx"]] - z["sample64"]).max() <= bound
+    idx, best = O.argmax(v)
+    assert np.abs(best - z["max64"]).max() <= bound
+    # argmax bit-exact wherever the reference's top-2 gap exceeds the rounding band
+    clear = z["gap64"] > 2 * bound
+    assert clear.mean() > 0.5
+    assert np.array_equal(idx[clear], z["argmax64"][clear].astype(np.int64))
+    g = np.ones_like(v)
+    dc, dp = O.backward_f64(g, cam, proj, k)
+    mg = max(1.0, np.abs(z["cg64"]).max())
+    assert np.abs(dc - z["cg64"]).max() <= 1e-7 * mg
+    assert np.abs(dp - z["pg64"]).max() <= 1e-7 * max(1.0, np.abs(z["pg64"]).max())
+
+
+def test_window_is_slice_of_full():
+    z, cam, proj, k, _ = _load(os.path.join(GOLD, "tex_24x48_k5.npz"))
+    D = 7
+    full = O.forward(cam, proj, k)
+    win = O.forward(cam, proj, k, layout=O.WINDOW, D=D)
+    H, W = cam.shape
+    for w in range(W - D):
+        assert np.array_equal(win[:, w, :], full[:, w, w:w + D + 1])
+
+
+def test_window_backward_matches_masked_full():
+    z, cam, proj, k, _ = _load(os.path.join(GOLD, "tiny_16x24_k5.npz"))
+    H, W = cam.shape
+    D = 5
+    rng = np.random.default_rng(3)
+    gw = rng.standard_normal((H, W - D, D + 1)).astype(np.float32)
+    gf = np.zeros((H, W, W), np.float32)
+    for w in range(W - D):
+        gf[:, w, w:w + D + 1] = gw[:, w, :]
+    a = O.backward_f64(gw, cam, proj, k, layout=O.WINDOW, D=D)
+    b = O.backward_f64(gf, cam, proj, k)
+    for x, y in zip(a, b):
+        assert np.abs(x - y).max() <= 1e-9 * max(1, np.abs(y).max())
+
+
+def test_constant_and_zero_images():
+    for v in (0.0, 0.5):
+        a = np.full((9, 13), v, np.float32)
+        out = O.forward(a, a, 3)
+        # interior patches are flat: E = 0, X = Y = 0 -> eps / sqrt(eps)
+        expect = np.float32(1e-8) / np.sqrt(np.float32(1e-8))
+        inner = out[1:-1, 1:-1, 1:-1] if v else out
+        assert np.abs(inner - expect).max() < 1e-9 + 1e-6 * abs(expect)
+
+
+def test_argmax_first_index_on_ties():
+    v = np.array([[1, 3, 3, 2], [0, 0, 0, 0]], np.float32)
+    idx, best = O.argmax(v)
+    assert idx.tolist() == [1, 0] and best.tolist() == [3, 0]
