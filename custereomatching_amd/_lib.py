@@ -20,7 +20,8 @@ OP_FORWARD, OP_BACKWARD, OP_DISPARITY = 0, 1, 2
 E_ARG, E_NULL, E_WORKSPACE, E_LAUNCH, E_UNSUPPORTED = -1, -2, -3, -4, -5
 
 EXPORTS = ("custma_abi_version", "custma_last_error", "custma_volume_dims", "custma_workspace_bytes",
-           "custma_forward", "custma_backward", "custma_argmax", "custma_disparity")
+           "custma_forward", "custma_backward", "custma_argmax", "custma_disparity", "custma_forward_band",
+           "custma_backward_band", "custma_disparity_band")
 
 
 class CustmaError(RuntimeError):
@@ -44,8 +45,12 @@ def _load():
     lib.custma_backward.argtypes = [vp, vp, vp, i32, i64, i64, i32, i32, i32, vp, vp, vp, sz, vp]
     lib.custma_argmax.argtypes = [vp, i64, i64, vp, vp, vp]
     lib.custma_disparity.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, vp, vp, vp, vp, sz, vp]
+    lib.custma_forward_band.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i32, i64, i64, vp, vp, sz, vp]
+    lib.custma_backward_band.argtypes = [vp, vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, vp, vp, vp, sz, vp]
+    lib.custma_disparity_band.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, vp, vp, vp, vp, sz,
+                                          vp]
     for name in ("custma_forward", "custma_backward", "custma_argmax", "custma_disparity",
-                 "custma_volume_dims"):
+                 "custma_volume_dims", "custma_forward_band", "custma_backward_band", "custma_disparity_band"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
 

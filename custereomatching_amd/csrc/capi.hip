@@ -47,6 +47,17 @@ int make_geo(int64_t H, int64_t W, int32_t k, int32_t layout, int32_t D, Geo* g)
     g->D = layout == CUSTMA_LAYOUT_WINDOW ? D : 0;
     g->WO = layout == CUSTMA_LAYOUT_WINDOW ? W - D : W;
     g->DO = layout == CUSTMA_LAYOUT_WINDOW ? (int64_t)D + 1 : W;
+    g->h_lo = 0;
+    g->h_hi = H;
+    return CUSTMA_OK;
+}
+
+int set_band(Geo* g, int64_t row_begin, int64_t row_end) {
+    if (row_begin < 0 || row_end > g->H || row_begin > row_end)
+        return fail(CUSTMA_E_ARG, "volume rows [%lld, %lld) must lie inside the image's %lld rows",
+                    (long long)row_begin, (long long)row_end, (long long)g->H);
+    g->h_lo = row_begin;
+    g->h_hi = row_end;
     return CUSTMA_OK;
 }
 
@@ -121,12 +132,20 @@ size_t custma_workspace_bytes(int64_t H, int64_t W, int32_t kernel_size, int32_t
 int custma_forward(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
                    int32_t kernel_size, int32_t layout, int32_t D, int32_t precision, float* cost_volume,
                    void* workspace, size_t workspace_bytes, void* stream) {
+    return custma_forward_band(camera, projector, dtype, H, W, kernel_size, layout, D, precision, 0, H, cost_volume,
+                               workspace, workspace_bytes, stream);
+}
+
+int custma_forward_band(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                        int32_t kernel_size, int32_t layout, int32_t D, int32_t precision, int64_t row_begin,
+                        int64_t row_end, float* cost_volume, void* workspace, size_t workspace_bytes,
+                        void* stream) {
     Geo g;
     int rc = make_geo(H, W, kernel_size, layout, D, &g);
-    if (rc || (rc = check_dtype(dtype))) return rc;
+    if (rc || (rc = check_dtype(dtype)) || (rc = set_band(&g, row_begin, row_end))) return rc;
     if (precision != CUSTMA_EXACT && precision != CUSTMA_FAST)
         return fail(CUSTMA_E_ARG, "unknown precision %d", precision);
-    if (g.H == 0 || g.W == 0) return CUSTMA_OK;
+    if (g.HV() == 0 || g.W == 0) return CUSTMA_OK;
     if (!camera || !projector || !cost_volume || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
     if (workspace_bytes < stats_bytes(g)) return fail(CUSTMA_E_WORKSPACE, "workspace too small");
     hipStream_t s = (hipStream_t)stream;
@@ -140,12 +159,27 @@ int custma_forward(const void* camera, const void* projector, int32_t dtype, int
 int custma_backward(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
                     int64_t W, int32_t kernel_size, int32_t layout, int32_t D, float* camera_grad,
                     float* projector_grad, void* workspace, size_t workspace_bytes, void* stream) {
+    return custma_backward_band(grad, camera, projector, dtype, H, W, kernel_size, layout, D, 0, H, camera_grad,
+                                projector_grad, workspace, workspace_bytes, stream);
+}
+
+int custma_backward_band(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
+                         int64_t W, int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin,
+                         int64_t row_end, float* camera_grad, float* projector_grad, void* workspace,
+                         size_t workspace_bytes, void* stream) {
     Geo g;
     int rc = make_geo(H, W, kernel_size, layout, D, &g);
-    if (rc || (rc = check_dtype(dtype))) return rc;
+    if (rc || (rc = check_dtype(dtype)) || (rc = set_band(&g, row_begin, row_end))) return rc;
     if (!fast_supported(g.k))
         return fail(CUSTMA_E_UNSUPPORTED, "backward supports odd kernel_size <= 15, got %d", g.k);
     if (g.H == 0 || g.W == 0 || (!camera_grad && !projector_grad)) return CUSTMA_OK;
+    if (g.HV() == 0) {  // no volume rows: gradients are zero
+        hipStream_t s0 = (hipStream_t)stream;
+        if (camera_grad) rc = check_hip(hipMemsetAsync(camera_grad, 0, sizeof(float) * g.H * g.W, s0), "memset");
+        if (!rc && projector_grad)
+            rc = check_hip(hipMemsetAsync(projector_grad, 0, sizeof(float) * g.H * g.W, s0), "memset");
+        return rc;
+    }
     if (!grad || !camera || !projector || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
     const size_t need = stats_bytes(g) + align256(backward_partial_bytes(g)) +
                         (projector_grad ? align256(backward_transpose_bytes(g)) : 0);
@@ -169,10 +203,18 @@ int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, 
 int custma_disparity(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
                      int32_t kernel_size, int32_t layout, int32_t D, int64_t* index, float* best,
                      int32_t* n_rechecked, void* workspace, size_t workspace_bytes, void* stream) {
+    return custma_disparity_band(camera, projector, dtype, H, W, kernel_size, layout, D, 0, H, index, best,
+                                 n_rechecked, workspace, workspace_bytes, stream);
+}
+
+int custma_disparity_band(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                          int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin, int64_t row_end,
+                          int64_t* index, float* best, int32_t* n_rechecked, void* workspace,
+                          size_t workspace_bytes, void* stream) {
     Geo g;
     int rc = make_geo(H, W, kernel_size, layout, D, &g);
-    if (rc || (rc = check_dtype(dtype))) return rc;
-    if (g.H == 0 || g.W == 0) return CUSTMA_OK;
+    if (rc || (rc = check_dtype(dtype)) || (rc = set_band(&g, row_begin, row_end))) return rc;
+    if (g.HV() == 0 || g.W == 0) return CUSTMA_OK;
     if (!camera || !projector || !index || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
     if (workspace_bytes < stats_bytes(g) + align256(disparity_partial_bytes(g)))
         return fail(CUSTMA_E_WORKSPACE, "workspace too small");

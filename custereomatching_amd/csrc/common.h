@@ -20,7 +20,9 @@ struct Geo {
     int32_t k, r;   // kernel size, radius
     int32_t layout; // CUSTMA_LAYOUT_*
     int32_t D;
-    int64_t WO, DO; // volume [H, WO, DO]
+    int64_t WO, DO; // volume [h_hi - h_lo, WO, DO]
+    int64_t h_lo, h_hi;  // volume rows = image rows [h_lo, h_hi) (row bands: the rest is halo)
+    __host__ __device__ int64_t HV() const { return h_hi - h_lo; }
 };
 
 // Per-image statistics produced by the stats pass ([H*W] each).
@@ -59,7 +61,7 @@ __device__ __forceinline__ bool voxel_valid(const Geo& g, int64_t w, int64_t d) 
 }
 __device__ __forceinline__ int64_t voxel_index(const Geo& g, int64_t h, int64_t w, int64_t d) {
     const int64_t s = (g.layout == CUSTMA_LAYOUT_WINDOW) ? d - w : d;
-    return (h * g.WO + w) * g.DO + s;
+    return ((h - g.h_lo) * g.WO + w) * g.DO + s;
 }
 
 }  // namespace custma

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void k_fwd_exact(const T* __restrict__ cam, co
     const int64_t b = blockIdx.x;
     const int dc = (int)(b % nDC);
     const int wt = (int)((b / nDC) % nWT);
-    const int64_t h = b / ((int64_t)nDC * nWT);
+    const int64_t h = g.h_lo + b / ((int64_t)nDC * nWT);
     const int64_t w0 = (int64_t)wt * TWX;
     const int64_t dA = (g.layout == CUSTMA_LAYOUT_WINDOW ? w0 : 0) + (int64_t)dc * TDX;
 
@@ -139,7 +139,7 @@ hipError_t launch_fwd_exact(const void* cam, const void* proj, int dtype, const 
                             float* out, hipStream_t s) {
     const int nWT = (int)cdiv(g.WO, TWX);
     const int nDC = (int)(g.layout == CUSTMA_LAYOUT_WINDOW ? cdiv(TWX + g.D, TDX) : cdiv(g.W, TDX));
-    const int64_t blocks = g.H * nWT * nDC;
+    const int64_t blocks = g.HV() * nWT * nDC;
     const size_t lds = sizeof(float) * (g.k * (TWX + 2 * g.r) + g.k * (TDX + 2 * g.r) + 2 * TWX + 2 * TDX);
     if (dtype == CUSTMA_F16)
         hipLaunchKernelGGL(k_fwd_exact<__half>, dim3((unsigned)blocks), dim3(256), lds, s, (const __half*)cam,

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, c
                                                     int64_t* __restrict__ idx, float* __restrict__ best,
                                                     int32_t* __restrict__ counter, int64_t* __restrict__ queue) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t npix = g.H * g.WO;
+    const int64_t npix = g.HV() * g.WO;
     if (p >= npix) return;
     float b = -FLT_MAX, sec = -FLT_MAX;
     int64_t bi = INT64_MAX;
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, c
             sec = fmaxf(sec, ob);
         }
     }
-    const int64_t h = p / g.WO, w = p % g.WO;
+    const int64_t h = g.h_lo + p / g.WO, w = p % g.WO;
     if (bi != INT64_MAX && (sec == -FLT_MAX || b - sec > tau)) {
         idx[p] = bi;
         if (best) best[p] = exact_cost(cam, proj, g, sc, sp, h, w, d_of_s(g, w, bi));
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void k_disp_recheck(const T* __restrict__ cam,
     const int n = *counter;
     for (int64_t e = blockIdx.x; e < n; e += gridDim.x) {
         const int64_t p = queue[e];
-        const int64_t h = p / g.WO, w = p % g.WO;
+        const int64_t h = g.h_lo + p / g.WO, w = p % g.WO;
         float bv = -INFINITY;
         int64_t bi = INT64_MAX;
         for (int64_t s = threadIdx.x; s < g.DO; s += blockDim.x) {
@@ -155,19 +155,19 @@ hipError_t launch_argmax(const float* vol, int64_t rows, int64_t n, int64_t* idx
 
 size_t disparity_partial_bytes(const Geo& g) {
     const SweepGrid sg = sweep_grid(g);
-    const size_t n = (size_t)sg.nChunk * g.H * g.WO;
-    return n * (4 + 4 + 4) + (size_t)g.H * g.WO * 8 + 256;
+    const size_t n = (size_t)sg.nChunk * g.HV() * g.WO;
+    return n * (4 + 4 + 4) + (size_t)g.HV() * g.WO * 8 + 256;
 }
 
 hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             int64_t* idx, float* best, int32_t* n_rechecked, void* ws, hipStream_t s) {
     const SweepGrid sg = sweep_grid(g);
-    const size_t n = (size_t)sg.nChunk * g.H * g.WO;
+    const size_t n = (size_t)sg.nChunk * g.HV() * g.WO;
     char* p = (char*)ws;
     int32_t* counter = (int32_t*)p;  // 256 B header
     p += 256;
     int64_t* queue = (int64_t*)p;
-    p += (size_t)g.H * g.WO * 8;
+    p += (size_t)g.HV() * g.WO * 8;
     DispPartial part;
     part.best = (float*)p;
     part.second = part.best + n;
@@ -182,7 +182,7 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
     }
     // certification margin: 2 x twice the fast path's worst-case error
     const float tau = (float)(8.0 * (g.k * g.k + 6) * 5.9604644775390625e-08);
-    const int64_t npix = g.H * g.WO;
+    const int64_t npix = g.HV() * g.WO;
     const unsigned mb = (unsigned)cdiv(npix, 256);
     if (dtype == CUSTMA_F16) {
         hipLaunchKernelGGL(k_disp_merge<__half>, dim3(mb), dim3(256), 0, s, (const __half*)cam, (const __half*)proj,

@@ -20,9 +20,9 @@ struct SweepGrid {
 };
 
 struct DispPartial {
-    float* best;     // [nChunk][H][WO]
-    float* second;   // [nChunk][H][WO]
-    int32_t* index;  // [nChunk][H][WO] layout index s of best, -1 if none
+    float* best;     // [nChunk][HV][WO]
+    float* second;   // [nChunk][HV][WO]
+    int32_t* index;  // [nChunk][HV][WO] layout index s of best, -1 if none
 };
 
 inline SweepGrid sweep_grid(const Geo& g) {
@@ -40,8 +40,8 @@ inline SweepGrid sweep_grid(const Geo& g) {
     sg.nTile = (int)cdiv(g.WO, TW);
     sg.TH = 64;
     // keep >= ~4 workgroups per CU on small problems
-    while (sg.TH > 8 && (int64_t)sg.nTile * sg.nChunk * cdiv(g.H, sg.TH) < 2048) sg.TH /= 2;
-    sg.nBand = (int)cdiv(g.H, sg.TH);
+    while (sg.TH > 8 && (int64_t)sg.nTile * sg.nChunk * cdiv(g.HV(), sg.TH) < 2048) sg.TH /= 2;
+    sg.nBand = (int)cdiv(g.HV(), sg.TH);
     return sg;
 }
 

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(320) void k_sweep_bwd(Geo g, Role ro, SweepGrid sg)
     };
     auto voxel_ok = [&](int64_t y, int64_t u) {
         const int64_t o = u + delta;
-        bool ok = y >= 0 && y < g.H && u >= 0 && u < ro.ownMax && o >= 0 && o < ro.othMax;
+        bool ok = y >= g.h_lo && y < g.h_hi && u >= 0 && u < ro.ownMax && o >= 0 && o < ro.othMax;
         if (ro.window) ok = ok && delta >= ro.dWinLo && delta <= ro.dWinHi;
         return ok;
     };
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(320) void k_sweep_bwd(Geo g, Role ro, SweepGrid sg)
         const int64_t u = xbase + x;
         if (!voxel_ok(y, u)) return 0.f;
         const int s = slot_of(y);
-        const float gv = ro.g[y * ro.gsH + u * ro.gsU + delta * ro.gsD + ro.gOff];
+        const float gv = ro.g[(y - g.h_lo) * ro.gsH + u * ro.gsU + delta * ro.gsD + ro.gOff];
         const float s2 = __builtin_fmaf(qU[s * NX + x], qO[s * NO + x + tid], kEps);
         return gv * __builtin_amdgcn_rsqf(s2);
     };
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void k_bwd_combine(Geo g, const T* __restrict_
 __global__ __launch_bounds__(256) void k_transpose_full(Geo g, const float* __restrict__ src,
                                                         float* __restrict__ dst) {
     __shared__ float t[32][33];
-    const int64_t h = blockIdx.z;
+    const int64_t h = blockIdx.z;  // volume row
     const int64_t bx = (int64_t)blockIdx.x * 32, by = (int64_t)blockIdx.y * 32;  // bx: d, by: w
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;                       // 32 x 8
     for (int i = ty; i < 32; i += 8) {
@@ -370,7 +370,7 @@ size_t backward_partial_bytes(const Geo& g) {
 }
 
 size_t backward_transpose_bytes(const Geo& g) {
-    return (size_t)g.H * g.W * (size_t)g.DO * sizeof(float);
+    return (size_t)g.HV() * g.W * (size_t)g.DO * sizeof(float);
 }
 
 hipError_t launch_backward(const float* grad, const void* cam, const void* proj, int dtype, const Geo& g,
@@ -407,11 +407,11 @@ hipError_t launch_backward(const float* grad, const void* cam, const void* proj,
         } else {          // projector: own = projector, other = camera, delta' = w - d
             if (win) {
                 const unsigned lds_t = (unsigned)(sizeof(float) * 32 * g.DO);
-                hipLaunchKernelGGL(k_transpose_window, dim3((unsigned)cdiv(g.W, 32), (unsigned)g.H), dim3(256),
+                hipLaunchKernelGGL(k_transpose_window, dim3((unsigned)cdiv(g.W, 32), (unsigned)g.HV()), dim3(256),
                                    lds_t, s, g, grad, gT);
             } else {
                 hipLaunchKernelGGL(k_transpose_full, dim3((unsigned)cdiv(g.W, 32), (unsigned)cdiv(g.W, 32),
-                                   (unsigned)g.H), dim3(256), 0, s, g, grad, gT);
+                                   (unsigned)g.HV()), dim3(256), 0, s, g, grad, gT);
             }
             if ((e = hipGetLastError()) != hipSuccess) return e;
             ro.own = proj; ro.oth = cam; ro.so = sp; ro.st = sc;

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(320) void k_sweep_fwd(const T* __restrict__ cam, co
     const int wt = (int)(bid % sg.nTile);
     const int band = (int)(bid / sg.nTile);
     const int64_t u0 = (int64_t)wt * TW;
-    const int64_t h0 = (int64_t)band * sg.TH, h1 = min(g.H, h0 + sg.TH);
+    const int64_t h0 = g.h_lo + (int64_t)band * sg.TH, h1 = min(g.h_hi, h0 + sg.TH);
     const int64_t dlo = g.layout == CUSTMA_LAYOUT_WINDOW ? 0 : -(u0 + TW - 1);
     const int64_t dhi = g.layout == CUSTMA_LAYOUT_WINDOW ? g.D : g.W - 1 - u0;
     const int64_t d0 = dlo + (int64_t)chunk * NL;
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(320) void k_sweep_fwd(const T* __restrict__ cam, co
                 c = num / den;
                 if constexpr (!ARGMAX) {
                     const int64_t sidx = g.layout == CUSTMA_LAYOUT_WINDOW ? delta : o;
-                    out[(h * g.WO + u) * g.DO + sidx] = c;
+                    out[((h - g.h_lo) * g.WO + u) * g.DO + sidx] = c;
                 }
             }
             if constexpr (ARGMAX) red[m * NL + tid] = c;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(320) void k_sweep_fwd(const T* __restrict__ cam, co
             }
             const int64_t u = u0 + m;
             if (red_live && part_i == 0 && u < g.WO) {
-                const int64_t pidx = ((int64_t)chunk * g.H + h) * g.WO + u;
+                const int64_t pidx = ((int64_t)chunk * g.HV() + (h - g.h_lo)) * g.WO + u;
                 part.best[pidx] = best;
                 part.second[pidx] = second;
                 int64_t sidx = -1;

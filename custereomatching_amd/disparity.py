@@ -19,28 +19,32 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib
-from .stereo_matching_wrapper import _LAYOUTS, _check_input, _check_pair, _stream_ptr, _workspace
+from .stereo_matching_wrapper import _LAYOUTS, _check_input, _check_pair, _rows, _stream_ptr, _workspace
 
 
 def stereo_disparity(camera: torch.Tensor, projector: torch.Tensor, D: int, kernel_size: int,
-                     layout: str = "full", return_rechecked: bool = False):
-    """(index [H, WO] int64, best cost [H, WO] fp32) without materialising the volume."""
+                     layout: str = "full", return_rechecked: bool = False,
+                     rows: Optional[Tuple[int, int]] = None):
+    """(index [H, WO] int64, best cost [H, WO] fp32) without materialising the volume.
+    ``rows=(b, e)``: only rows [b, e) of a haloed row band."""
     code = _check_pair(camera, projector, kernel_size)
     lay = _LAYOUTS[layout]
     H, W = camera.shape
+    r0, r1 = _rows(H, rows)
     Dl = int(D) if lay == _lib.LAYOUT_WINDOW else 0
     WO, _ = _lib.volume_dims(H, W, lay, Dl)
     dev = camera.device
-    idx = torch.empty((H, WO), dtype=torch.int64, device=dev)
-    best = torch.empty((H, WO), dtype=torch.float32, device=dev)
+    idx = torch.empty((r1 - r0, WO), dtype=torch.int64, device=dev)
+    best = torch.empty((r1 - r0, WO), dtype=torch.float32, device=dev)
     nre = torch.zeros(1, dtype=torch.int32, device=dev)
     if idx.numel():
         with torch.cuda.device(dev):
             nb = _lib.workspace_bytes(H, W, kernel_size, lay, Dl, _lib.OP_DISPARITY)
             ws = _workspace(nb, dev)
-            _lib.check(_lib.lib.custma_disparity(camera.data_ptr(), projector.data_ptr(), code, H, W, kernel_size,
-                                                 lay, Dl, idx.data_ptr(), best.data_ptr(), nre.data_ptr(),
-                                                 ws.data_ptr(), ws.numel(), _stream_ptr(dev)), "stereo_disparity")
+            _lib.check(_lib.lib.custma_disparity_band(camera.data_ptr(), projector.data_ptr(), code, H, W,
+                                                      kernel_size, lay, Dl, r0, r1, idx.data_ptr(), best.data_ptr(),
+                                                      nre.data_ptr(), ws.data_ptr(), ws.numel(), _stream_ptr(dev)),
+                       "stereo_disparity")
     if return_rechecked:
         return idx, best, nre
     return idx, best

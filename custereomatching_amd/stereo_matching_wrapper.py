@@ -91,43 +91,60 @@ def _workspace(nbytes: int, dev: torch.device) -> torch.Tensor:
     return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
 
 
+def _rows(H: int, rows: Optional[Tuple[int, int]]) -> Tuple[int, int]:
+    if rows is None:
+        return 0, H
+    r0, r1 = int(rows[0]), int(rows[1])
+    if not 0 <= r0 <= r1 <= H:
+        raise ValueError(f"rows {rows} must satisfy 0 <= begin <= end <= {H}")
+    return r0, r1
+
+
 def cost_volume_forward(camera: torch.Tensor, projector: torch.Tensor, D: int, kernel_size: int,
-                        layout: str = "full", precision: Optional[str] = None) -> torch.Tensor:
+                        layout: str = "full", precision: Optional[str] = None,
+                        rows: Optional[Tuple[int, int]] = None) -> torch.Tensor:
     """Forward volume without autograd (reference: stereo::stereo_matching_forward,
-    custma/src/stereo_matching.cpp:16-42)."""
+    custma/src/stereo_matching.cpp:16-42).  ``rows=(b, e)`` computes only volume
+    rows [b, e) of a haloed row band (custma_forward_band)."""
     code = _check_pair(camera, projector, kernel_size)
     lay = _LAYOUTS[layout]
     prec = _PRECISIONS[precision or default_precision()]
     H, W = camera.shape
+    r0, r1 = _rows(H, rows)
     D = int(D)
     Dl = D if lay == _lib.LAYOUT_WINDOW else 0
     WO, DO = _lib.volume_dims(H, W, lay, Dl)
     dev = camera.device
-    out = torch.empty((H, WO, DO), dtype=torch.float32, device=dev)
+    out = torch.empty((r1 - r0, WO, DO), dtype=torch.float32, device=dev)
     if out.numel() == 0:
         return out
     with torch.cuda.device(dev):
         nb = _lib.workspace_bytes(H, W, kernel_size, lay, Dl, _lib.OP_FORWARD)
         ws = _workspace(nb, dev)
-        _lib.check(_lib.lib.custma_forward(camera.data_ptr(), projector.data_ptr(), code, H, W, kernel_size, lay,
-                                           Dl, prec, out.data_ptr(), ws.data_ptr(), ws.numel(),
-                                           _stream_ptr(dev)), "stereo_matching_forward")
+        _lib.check(_lib.lib.custma_forward_band(camera.data_ptr(), projector.data_ptr(), code, H, W, kernel_size,
+                                                lay, Dl, prec, r0, r1, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                _stream_ptr(dev)), "stereo_matching_forward")
     return out
 
 
 def cost_volume_backward(cost_volume_grad: torch.Tensor, camera: torch.Tensor, projector: torch.Tensor,
                          kernel_size: int, layout: str = "full", D: int = 0, camera_grad: bool = True,
-                         projector_grad: bool = False) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+                         projector_grad: bool = False, rows: Optional[Tuple[int, int]] = None
+                         ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
     """Gradients of sum(grad * volume) (reference: stereo::stereo_matching_backward,
-    custma/src/stereo_matching.cpp:45-73; camera only there)."""
+    custma/src/stereo_matching.cpp:45-73; camera only there).  With ``rows=(b, e)``
+    the grad covers volume rows [b, e) of a haloed band and the returned image
+    gradients cover every buffer row (halo rows hold partial sums)."""
     _check_input(cost_volume_grad, "cost_volume_grad")
     code = _check_pair(camera, projector, kernel_size)
     lay = _LAYOUTS[layout]
     H, W = camera.shape
+    r0, r1 = _rows(H, rows)
     Dl = int(D) if lay == _lib.LAYOUT_WINDOW else 0
     WO, DO = _lib.volume_dims(H, W, lay, Dl)
-    if tuple(cost_volume_grad.shape) != (H, WO, DO):
-        raise RuntimeError(f"cost_volume_grad shape {tuple(cost_volume_grad.shape)} != volume shape {(H, WO, DO)}")
+    if tuple(cost_volume_grad.shape) != (r1 - r0, WO, DO):
+        raise RuntimeError(f"cost_volume_grad shape {tuple(cost_volume_grad.shape)} != volume shape "
+                           f"{(r1 - r0, WO, DO)}")
     if cost_volume_grad.dtype != torch.float32:
         raise RuntimeError(f"expected scalar type Float but found {cost_volume_grad.dtype}")
     dev = camera.device
@@ -138,8 +155,8 @@ def cost_volume_backward(cost_volume_grad: torch.Tensor, camera: torch.Tensor, p
     with torch.cuda.device(dev):
         nb = _lib.workspace_bytes(H, W, kernel_size, lay, Dl, _lib.OP_BACKWARD)
         ws = _workspace(nb, dev)
-        _lib.check(_lib.lib.custma_backward(cost_volume_grad.data_ptr(), camera.data_ptr(), projector.data_ptr(),
-                                            code, H, W, kernel_size, lay, Dl,
+        _lib.check(_lib.lib.custma_backward_band(cost_volume_grad.data_ptr(), camera.data_ptr(),
+                                                 projector.data_ptr(), code, H, W, kernel_size, lay, Dl, r0, r1,
                                             gc.data_ptr() if gc is not None else None,
                                             gp.data_ptr() if gp is not None else None,
                                             ws.data_ptr(), ws.numel(), _stream_ptr(dev)),

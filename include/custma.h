@@ -82,6 +82,24 @@ int custma_backward(const float* grad, const void* camera, const void* projector
                     int64_t W, int32_t kernel_size, int32_t layout, int32_t D, float* camera_grad,
                     float* projector_grad, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Row-band variants (multi-GPU row sharding): the image buffers hold H rows -- a band plus
+ * its halo -- and only volume rows [row_begin, row_end) are produced / consumed.  The volume (and grad)
+ * has row_end - row_begin rows; patches of those rows read the halo rows, and zero padding applies only
+ * at the buffer's edges (= the global image's edges when the band has no halo there).  The backward
+ * writes gradients for all H buffer rows: the halo rows hold partial sums a neighbour must add. */
+int custma_forward_band(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                        int32_t kernel_size, int32_t layout, int32_t D, int32_t precision, int64_t row_begin,
+                        int64_t row_end, float* cost_volume, void* workspace, size_t workspace_bytes,
+                        void* stream);
+int custma_backward_band(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
+                         int64_t W, int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin,
+                         int64_t row_end, float* camera_grad, float* projector_grad, void* workspace,
+                         size_t workspace_bytes, void* stream);
+int custma_disparity_band(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                          int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin, int64_t row_end,
+                          int64_t* index, float* best, int32_t* n_rechecked, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
 /* First-index argmax over the last axis of a [rows, n] fp32 array (torch.argmax semantics), as the
  * reference's callers do on the volume (examples/verify.py:72, examples/test.py:78-83). */
 int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, float* best, void* stream);

@@ -278,3 +278,37 @@ def test_large_backward_band_vs_oracle(gpu):
     rc, rp = rc[h0 - a0:h1 - a0], rp[h0 - a0:h1 - a0]
     assert np.abs(gc[h0:h1].cpu().numpy() - rc).max() <= 1e-5 * max(1, np.abs(rc).max())
     assert np.abs(gp[h0:h1].cpu().numpy() - rp).max() <= 1e-5 * max(1, np.abs(rp).max())
+
+
+@pytest.mark.parametrize("layout,D", [(FULL, 0), (WIN, 12)])
+def test_band_api_matches_whole_image(gpu, layout, D):
+    """custma_*_band: volume rows [b, e) of a haloed buffer equal the whole-image
+    volume's rows; band gradients + halo partials add up to the whole-image gradient."""
+    H, W, k = 40, 48, 7
+    r = k // 2
+    cam, proj = make_pair(H, W, 16, seed=44)
+    c, p = _dev(cam, gpu), _dev(proj, gpu)
+    full = cm.cost_volume_forward(c, p, D, k, layout, "exact")
+    g = _dev(_rand_grad(tuple(full.shape), 45), gpu)
+    rc, rp = cm.cost_volume_backward(g, c, p, k, layout, D, projector_grad=True)
+    # two bands: rows [0, 17) and [17, 40), buffers with r halo rows
+    acc_c = torch.zeros_like(rc)
+    acc_p = torch.zeros_like(rp)
+    for b, e in ((0, 17), (17, 40)):
+        a0, a1 = max(0, b - r), min(H, e + r)
+        vb = cm.cost_volume_forward(c[a0:a1].contiguous(), p[a0:a1].contiguous(), D, k, layout, "exact",
+                                    rows=(b - a0, e - a0))
+        assert torch.equal(vb, full[b:e])
+        fb = cm.cost_volume_forward(c[a0:a1].contiguous(), p[a0:a1].contiguous(), D, k, layout, "fast",
+                                    rows=(b - a0, e - a0))
+        assert float((fb - full[b:e]).abs().max()) <= O.cost_error_bound(k)
+        gc, gp = cm.cost_volume_backward(g[b:e].contiguous(), c[a0:a1].contiguous(), p[a0:a1].contiguous(), k,
+                                         layout, D, projector_grad=True, rows=(b - a0, e - a0))
+        acc_c[a0:a1] += gc
+        acc_p[a0:a1] += gp
+        ib, bb = cm.stereo_disparity(c[a0:a1].contiguous(), p[a0:a1].contiguous(), D, k, layout,
+                                     rows=(b - a0, e - a0))
+        vi, vb2 = cm.volume_argmax(full[b:e].contiguous())
+        assert torch.equal(ib, vi) and torch.equal(bb, vb2)
+    assert float((acc_c - rc).abs().max()) <= 1e-5 * max(1.0, float(rc.abs().max()))
+    assert float((acc_p - rp).abs().max()) <= 1e-5 * max(1.0, float(rp.abs().max()))
