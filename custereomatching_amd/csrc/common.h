@@ -53,6 +53,16 @@ __device__ __forceinline__ float ldpad(const T* img, int64_t H, int64_t W, int64
 
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// XCD-aware block order.  Workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, "Workgroup dispatch"): hardware block b runs on XCD
+// b % 8.  Map it to a logical block so that each XCD gets one contiguous range
+// of logical blocks (bijective for any grid size); neighbouring logical blocks
+// then share an L2.  Only speed depends on this, never correctness.
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
+    const int64_t q = nb / 8, rem = nb % 8, x = b % 8, i = b / 8;
+    return x < rem ? x * (q + 1) + i : rem * (q + 1) + (x - rem) * q + i;
+}
+
 // Volume voxel validity and linear index for camera column w, projector column d.
 __device__ __forceinline__ bool voxel_valid(const Geo& g, int64_t w, int64_t d) {
     if (w < 0 || w >= g.WO || d < 0 || d >= g.W) return false;
@@ -62,6 +72,30 @@ __device__ __forceinline__ bool voxel_valid(const Geo& g, int64_t w, int64_t d) 
 __device__ __forceinline__ int64_t voxel_index(const Geo& g, int64_t h, int64_t w, int64_t d) {
     const int64_t s = (g.layout == CUSTMA_LAYOUT_WINDOW) ? d - w : d;
     return ((h - g.h_lo) * g.WO + w) * g.DO + s;
+}
+
+// Raw buffer access (MI355X: 128-bit descriptor in SGPRs, 32-bit per-lane byte
+// offset, hardware range check).  An out-of-range offset (0x80000000) makes a
+// load return 0 and a store a no-op -- branch-free zero padding / masking.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ float ld_buf(__amdgpu_buffer_rsrc_t r, uint32_t off);
+template <>
+__device__ __forceinline__ float ld_buf<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+template <>
+__device__ __forceinline__ float ld_buf<__half>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const unsigned short b = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+    return __half2float(__ushort_as_half(b));
+}
+__device__ __forceinline__ double ld_buf_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ void st_buf(float v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, 0);
 }
 
 }  // namespace custma

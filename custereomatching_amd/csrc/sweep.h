@@ -1,5 +1,7 @@
 // Shared geometry of the sliding-window ("sweep") kernels.
 #pragma once
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace custma {
@@ -16,7 +18,8 @@ struct SweepGrid {
     int nTile;   // column tiles of TW
     int nBand;   // row bands
     int TH;      // rows per band
-    int NL;      // lanes (diagonals) per workgroup = blockDim.x
+    int NL;      // lanes per workgroup = blockDim.x
+    int TD;      // diagonals per lane (forward sweep); a chunk covers TD * NL diagonals
 };
 
 struct DispPartial {
@@ -25,18 +28,28 @@ struct DispPartial {
     int32_t* index;  // [nChunk][HV][WO] layout index s of best, -1 if none
 };
 
-inline SweepGrid sweep_grid(const Geo& g) {
+// Lane / chunk geometry.  td_max = 2 for the forward sweep (two diagonals
+// per lane), 1 for the backward.  The diagonal range of a column tile is
+// split into chunks of TD * NL; the choice minimises idle lanes.
+inline SweepGrid sweep_grid(const Geo& g, int td_max = 1) {
     SweepGrid sg;
-    if (g.layout == CUSTMA_LAYOUT_WINDOW) {
-        const int64_t nd = (int64_t)g.D + 1;
-        int nw = (int)cdiv(nd, 64);
-        if (nw > 5) nw = 4;
-        sg.NL = 64 * nw;
-        sg.nChunk = (int)cdiv(nd, sg.NL);
-    } else {
-        sg.NL = 256;
-        sg.nChunk = (int)cdiv(g.W + TW - 1, sg.NL);
-    }
+    const int64_t nd = g.layout == CUSTMA_LAYOUT_WINDOW ? (int64_t)g.D + 1 : g.W + TW - 1;
+    // cost = diagonal slots launched, discounted for two diagonals per lane (half the LDS
+    // bytes per voxel) and penalised for single-wave workgroups
+    double best = 1e300;
+    sg.NL = 256; sg.TD = 1;
+    // tuning overrides (benchmarking only): CUSTMA_SWEEP_TD, CUSTMA_SWEEP_NW
+    const char* etd = getenv("CUSTMA_SWEEP_TD");
+    const char* enw = getenv("CUSTMA_SWEEP_NW");
+    const int td_fix = etd ? atoi(etd) : 0, nw_fix = enw ? atoi(enw) : 0;
+    for (int td = 1; td <= td_max; ++td)
+        for (int nw = 1; nw <= (g.layout == CUSTMA_LAYOUT_WINDOW ? 5 : 4); ++nw) {
+            if ((td_fix && td != td_fix) || (nw_fix && nw != nw_fix)) continue;
+            const int64_t per = (int64_t)64 * nw * td;
+            const double cost = (double)(cdiv(nd, per) * per) * (td == 2 ? 0.8 : 1.0) * (nw == 1 ? 1.1 : 1.0);
+            if (cost < best) { best = cost; sg.NL = 64 * nw; sg.TD = td; }
+        }
+    sg.nChunk = (int)cdiv(nd, (int64_t)sg.NL * sg.TD);
     sg.nTile = (int)cdiv(g.WO, TW);
     sg.TH = 64;
     // keep >= ~4 workgroups per CU on small problems

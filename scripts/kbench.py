@@ -1,0 +1,61 @@
+"""Quick per-op timing (HIP events) for kernel iteration. Not the contract bench."""
+import argparse, json, os, sys, time
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import custereomatching_amd as cm
+from bench import synth_pair, EventTimer
+
+CFGS = {
+    "c2_full": dict(H=1024, W=1024, k=9, D=128, layout="full", dtype=torch.float32),
+    "c2_win": dict(H=1024, W=1024, k=9, D=128, layout="window", dtype=torch.float32),
+    "c3_win": dict(H=2048, W=2048, k=11, D=256, layout="window", dtype=torch.float16),
+    "c3_full": dict(H=2048, W=2048, k=11, D=256, layout="full", dtype=torch.float16),
+}
+
+def run(name, ops, reps):
+    c = CFGS[name]
+    H, W, k, D, lay, dt = c["H"], c["W"], c["k"], c["D"], c["layout"], c["dtype"]
+    cam, proj = synth_pair(H, W, D, 5, "cuda", dt)
+    res = {"cfg": name}
+    if "fwd" in ops or "exact" in ops:
+        for prec in [p for p in ("fast", "exact") if (p == "fast" and "fwd" in ops) or (p == "exact" and "exact" in ops)]:
+            out = cm.cost_volume_forward(cam, proj, D, k, lay, prec)
+            et = EventTimer()
+            for _ in range(reps):
+                et.record(lambda: cm.cost_volume_forward(cam, proj, D, k, lay, prec, ))
+            ms = et.mean_ms()
+            nb = out.numel() * 4 + 2 * H * W * cam.element_size()
+            res[f"fwd_{prec}_ms"] = round(ms, 4)
+            res[f"fwd_{prec}_GBps"] = round(nb / ms / 1e6, 1)
+            del out
+    if "bwd" in ops:
+        WO = W if lay == "full" else W - D
+        DO = W if lay == "full" else D + 1
+        g = torch.rand(H, WO, DO, device="cuda") - 0.5
+        cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True)
+        et = EventTimer()
+        for _ in range(reps):
+            et.record(lambda: cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True))
+        ms = et.mean_ms()
+        res["bwd_ms"] = round(ms, 4)
+        res["bwd_GBps_g"] = round(g.numel() * 4 / ms / 1e6, 1)
+        del g
+    if "disp" in ops:
+        cm.stereo_disparity(cam, proj, D, k, lay)
+        et = EventTimer()
+        nre = None
+        for _ in range(reps):
+            nre = et.record(lambda: cm.stereo_disparity(cam, proj, D, k, lay, return_rechecked=True))
+        res["disp_ms"] = round(et.mean_ms(), 4)
+        res["disp_rechecked"] = int(nre[2].item())
+    torch.cuda.empty_cache()
+    return res
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", default="c2_full,c3_win")
+    ap.add_argument("--ops", default="fwd,bwd")
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    for n in a.cfg.split(","):
+        print(json.dumps(run(n, a.ops.split(","), a.reps)), flush=True)
