@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  -- must load torch's libamdhip64 before ours (same soname)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libcustma_hip.so")
+# CUSTMA_LIB selects another build of the same library (ablation builds, scripts/ablate.sh)
+LIB_PATH = os.environ.get("CUSTMA_LIB") or os.path.join(_HERE, "_lib", "libcustma_hip.so")
 
 F32, F16 = 0, 1
 LAYOUT_FULL, LAYOUT_WINDOW = 0, 1

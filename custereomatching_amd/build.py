@@ -33,9 +33,9 @@ def _deps():
         os.path.join(HERE, "..", "include", "custma.h")]
 
 
-def _compile(src):
-    out = _obj(src)
-    cmd = [HIPCC, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", out]
+def _compile(src, extra=(), libdir=LIBDIR):
+    out = os.path.join(libdir, os.path.splitext(src)[0] + ".o")
+    cmd = [HIPCC, *CFLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -56,6 +56,20 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if verbose:
         print("built", LIB)
     return LIB
+
+
+def build_variant(libdir: str, defines) -> str:
+    """Ablation build (benchmarking only): the same library compiled with extra
+    -D switches into another directory; load it with CUSTMA_LIB=<path>."""
+    os.makedirs(libdir, exist_ok=True)
+    extra = [f"-D{d}" for d in defines]
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, extra, libdir), SOURCES))
+    lib = os.path.join(libdir, "libcustma_hip.so")
+    r = subprocess.run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", lib, *objs], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return lib
 
 
 if __name__ == "__main__":

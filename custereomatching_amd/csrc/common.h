@@ -94,8 +94,11 @@ __device__ __forceinline__ float ld_buf<__half>(__amdgpu_buffer_rsrc_t r, uint32
 __device__ __forceinline__ double ld_buf_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
+#ifndef CUSTMA_STORE_AUX
+#define CUSTMA_STORE_AUX 0  // cache-policy bits of the volume stores (gfx950: 1 sc0, 2 nt, 16 sc1)
+#endif
 __device__ __forceinline__ void st_buf(float v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, CUSTMA_STORE_AUX);
 }
 
 }  // namespace custma

@@ -14,12 +14,12 @@ constexpr int TW = 16;  // camera (own-image) columns per workgroup
 #define CUSTMA_SWEEP_KS(X) X(1) X(3) X(5) X(7) X(9) X(11) X(13) X(15)
 
 struct SweepGrid {
-    int nChunk;  // disparity-diagonal chunks per column tile
+    int nChunk;  // diagonal chunks per column tile
     int nTile;   // column tiles of TW
     int nBand;   // row bands
     int TH;      // rows per band
-    int NL;      // lanes per workgroup = blockDim.x
-    int TD;      // diagonals per lane (forward sweep); a chunk covers TD * NL diagonals
+    int NL;      // diagonal lanes per workgroup (compute waves x 64)
+    int S;       // chunk stride in volume columns (== NL unless chunks own aligned columns)
 };
 
 struct DispPartial {
@@ -28,28 +28,44 @@ struct DispPartial {
     int32_t* index;  // [nChunk][HV][WO] layout index s of best, -1 if none
 };
 
-// Lane / chunk geometry.  td_max = 2 for the forward sweep (two diagonals
-// per lane), 1 for the backward.  The diagonal range of a column tile is
-// split into chunks of TD * NL; the choice minimises idle lanes.
-inline SweepGrid sweep_grid(const Geo& g, int td_max = 1) {
+// Lane / chunk geometry.
+//
+// owned = false: the diagonal range of a column tile is split into disjoint
+// chunks of NL (disparity partials, backward).
+// owned = true (volume stores): chunk c owns the columns [b_c, b_c+1) of every
+// volume row, b_c = the first column >= c*S that starts a 64-byte sector, so
+// every sector of the volume has one writer (two workgroups writing parts of
+// one sector halve the store bandwidth, scripts/micro/store_sim.hip).  A row
+// range of up to S+15 columns shifted by the 16 camera columns of the tile
+// (full layout) needs S + 15 (+15 when volume rows are not sector aligned)
+// diagonal lanes, so neighbouring chunks compute a few diagonals twice.
+inline int owned_margin(const Geo& g) {
+    if (g.layout == CUSTMA_LAYOUT_WINDOW) return 16;
+    return g.DO % 16 == 0 ? 16 : 32;
+}
+
+inline SweepGrid sweep_grid(const Geo& g, bool owned = false) {
     SweepGrid sg;
+    const int64_t ncol = g.DO;  // volume columns per row (full: W, window: D+1)
     const int64_t nd = g.layout == CUSTMA_LAYOUT_WINDOW ? (int64_t)g.D + 1 : g.W + TW - 1;
-    // cost = diagonal slots launched, discounted for two diagonals per lane (half the LDS
-    // bytes per voxel) and penalised for single-wave workgroups
+    const int margin = owned ? owned_margin(g) : 0;
+    // cost = diagonal lanes launched, penalised for single-wave workgroups
     double best = 1e300;
-    sg.NL = 256; sg.TD = 1;
-    // tuning overrides (benchmarking only): CUSTMA_SWEEP_TD, CUSTMA_SWEEP_NW
-    const char* etd = getenv("CUSTMA_SWEEP_TD");
+    sg.NL = 256;
+    // tuning override (benchmarking only): CUSTMA_SWEEP_NW
     const char* enw = getenv("CUSTMA_SWEEP_NW");
-    const int td_fix = etd ? atoi(etd) : 0, nw_fix = enw ? atoi(enw) : 0;
-    for (int td = 1; td <= td_max; ++td)
-        for (int nw = 1; nw <= (g.layout == CUSTMA_LAYOUT_WINDOW ? 5 : 4); ++nw) {
-            if ((td_fix && td != td_fix) || (nw_fix && nw != nw_fix)) continue;
-            const int64_t per = (int64_t)64 * nw * td;
-            const double cost = (double)(cdiv(nd, per) * per) * (td == 2 ? 0.8 : 1.0) * (nw == 1 ? 1.1 : 1.0);
-            if (cost < best) { best = cost; sg.NL = 64 * nw; sg.TD = td; }
-        }
-    sg.nChunk = (int)cdiv(nd, (int64_t)sg.NL * sg.TD);
+    const int nw_fix = enw ? atoi(enw) : 0;
+    for (int nw = 1; nw <= 5; ++nw) {
+        if (nw_fix && nw != nw_fix) continue;
+        if (owned && 64 * nw <= margin) continue;
+        if (!owned && g.layout != CUSTMA_LAYOUT_WINDOW && nw > 4) continue;
+        const int64_t per = owned ? 64 * nw - margin : 64 * nw;
+        const int64_t n = owned ? cdiv(ncol, per) : cdiv(nd, per);
+        const double cost = (double)(n * 64 * nw) * (nw == 1 ? 1.1 : 1.0) * (nw == 5 ? 1.05 : 1.0);
+        if (cost < best) { best = cost; sg.NL = 64 * nw; }
+    }
+    sg.S = owned ? sg.NL - margin : sg.NL;
+    sg.nChunk = (int)(owned ? cdiv(ncol, (int64_t)sg.S) : cdiv(nd, (int64_t)sg.NL));
     sg.nTile = (int)cdiv(g.WO, TW);
     sg.TH = 64;
     // keep >= ~4 workgroups per CU on small problems

@@ -353,7 +353,7 @@ hipError_t run_role(const Geo& g, const Role& ro, const SweepGrid& sg, hipStream
 }
 
 SweepGrid bwd_grid(const Geo& g) {
-    SweepGrid sg = sweep_grid(g, 1);
+    SweepGrid sg = sweep_grid(g);
     sg.nTile = (int)cdiv(g.W, TW);  // every own-image column needs its gradient
     sg.TH = 64;
     while (sg.TH > 8 && (int64_t)sg.nTile * sg.nChunk * cdiv(g.H, sg.TH) < 2048) sg.TH /= 2;

@@ -53,6 +53,8 @@ template <int L>
 __device__ __forceinline__ void fmac_bc32(float& acc, float a, float b) {
     asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(a), "v"(b), "i"(L));
 }
+typedef __attribute__((address_space(3))) volatile double lds_vd;
+
 template <int X, int NX>
 struct Unroll {
     template <typename F>
@@ -68,20 +70,21 @@ struct Unroll<NX, NX> {
 };
 
 template <int K, int TWT, typename T, bool ARGMAX>
-__global__ __launch_bounds__(320, 2) void k_sweep_fwd(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
-                                                      Stats sc, Stats sp, float* __restrict__ out, SweepGrid sg,
-                                                      DispPartial part) {
-    constexpr int R = K / 2, NX = TWT + 2 * R, NSLOT = K + 2;
+__global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
+                                                   Stats sc, Stats sp, float* __restrict__ out, SweepGrid sg,
+                                                   DispPartial part) {
+    constexpr int R = K / 2, NX = TWT + 2 * R;
     static_assert(TWT == 16 && NX <= 32, "row-broadcast layout assumes 16 own columns and <= 32 taps");
+    constexpr int NL_MAX = 320, LO = (NX + NL_MAX - 1 + 63) / 64, LS = (TWT + NL_MAX - 1 + 63) / 64;
     const int NL = sg.NL, NO = NX + NL - 1, NS = TWT + NL - 1;
     extern __shared__ __attribute__((aligned(16))) double ldsd[];
-    double* rsM = ldsd;                         // [2][NS]  projector fp64 patch means
-    double* usB = rsM + 2 * NS;                 // [2][16]  -(camera fp64 patch sums)
-    double* ringU = usB + 2 * 16;               // [NSLOT][2][32]  +c, -c of a camera row
-    double* ringO = ringU + NSLOT * 64;         // [NSLOT][NO] projector row
-    float* rsQ = (float*)(ringO + NSLOT * NO);  // [2][NS]  projector ey2
-    float* usQ = rsQ + 2 * NS;                  // [2][16]  camera ex2
-    float* red = usQ + 2 * 16;                  // [TWT][NL] (ARGMAX only)
+    double* ringO = ldsd;                  // [2 buf][2 enter/leave][NO] projector rows
+    double* ringU = ringO + 4 * NO;        // [2 buf][64]: +c of the entering row, -c of the leaving row
+    double* rsM = ringU + 2 * 64;          // [2][NS]  projector fp64 patch means
+    double* usB = rsM + 2 * NS;            // [2][16]  -(camera fp64 patch sums)
+    float* rsQ = (float*)(usB + 2 * 16);   // [2][NS]  projector ey2
+    float* usQ = rsQ + 2 * NS;             // [2][16]  camera ex2
+    float* stg = usQ + 2 * 16;             // [2][16][NL] cost tile staging (ARGMAX: [16][NL] reduction)
 
     const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
     const int chunk = (int)(bid % sg.nChunk);
@@ -90,225 +93,303 @@ __global__ __launch_bounds__(320, 2) void k_sweep_fwd(const T* __restrict__ cam,
     const int band = (int)(rest / sg.nTile);
     const int64_t u0 = (int64_t)wt * TWT;
     const int64_t h0 = g.h_lo + (int64_t)band * sg.TH, h1 = min(g.h_hi, h0 + sg.TH);
-    const int64_t dlo = g.layout == CUSTMA_LAYOUT_WINDOW ? 0 : -(u0 + TWT - 1);
-    const int64_t dhi = g.layout == CUSTMA_LAYOUT_WINDOW ? g.D : g.W - 1 - u0;
-    const int64_t d0 = dlo + (int64_t)chunk * NL;
+    const int64_t hs = h0 - 2 * R;  // first step: 2R warm-up steps fill the column sums
+    const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
+    const int64_t dlo = window ? 0 : -(u0 + TWT - 1);
+    const int64_t dhi = window ? g.D : g.W - 1 - u0;
+    const int64_t d0 = dlo + (int64_t)chunk * sg.S;
     const int tid = threadIdx.x;
-    const int64_t delta = d0 + tid;
+    // The last wave of the workgroup is the loader: it stages image rows and statistics
+    // into LDS a step ahead and never stores to HBM.  The other waves compute and store
+    // and never load from HBM.  (vmcnt counts loads and stores in issue order, so a wave
+    // doing both waits for its earlier volume stores whenever it consumes a load.)
+    const bool loader = __builtin_amdgcn_readfirstlane(tid) >= NL;
     const double rk2 = 1.0 / (double)(K * K);
+    constexpr uint32_t OOB = 0x80000000u;
 
-    // valid camera-column offsets m in [m_lo, m_hi) for this lane's diagonal
-    int m_lo = TWT, m_hi = 0;
+    if (loader) {
+        // ---- branch-free raw buffer loads (out-of-range -> 0 = the reference's zero
+        // padding, stereo_matching_kernel.cu:6-12): loop-invariant per-lane byte offsets,
+        // the row chosen by the descriptor (zero-size for rows outside the image) ----
+        const int li = tid - NL;
+        const int64_t xU0 = u0 - R, xO0 = u0 - R + d0, oS = u0 + d0;
+        auto colOff = [&](bool have, int64_t x, int esz) -> uint32_t {
+            return (have && x >= 0 && x < g.W) ? (uint32_t)(x * esz) : OOB;
+        };
+        auto row_rsrc = [&](const void* base, int64_t row, int esz, bool ok) {
+            ok = ok && row >= 0 && row < g.H;
+            return make_rsrc((const char*)base + (ok ? row : 0) * g.W * esz, ok ? (uint32_t)(g.W * esz) : 0u);
+        };
+        uint32_t vO[LO], vSd[LS], vSf[LS];
+        const uint32_t vUe = colOff(li < NX, xU0 + li, sizeof(T));
+        const uint32_t vUl = colOff(li >= 32 && li - 32 < NX, xU0 + li - 32, sizeof(T));
+        const uint32_t vUSd = colOff(li < TWT, u0 + li, 8), vUSf = colOff(li < TWT, u0 + li, 4);
+#pragma unroll
+        for (int j = 0; j < LO; ++j) vO[j] = colOff(li + 64 * j < NO, xO0 + li + 64 * j, sizeof(T));
+#pragma unroll
+        for (int j = 0; j < LS; ++j) {
+            vSd[j] = colOff(li + 64 * j < NS, oS + li + 64 * j, 8);
+            vSf[j] = colOff(li + 64 * j < NS, oS + li + 64 * j, 4);
+        }
+        struct Stage {
+            float ue, ul, oe[LO], ol[LO], q[LS], uq;
+            double m[LS], ub;
+        };
+        // step t adds image row t+R and removes row t-R-1 (once it was added: rows from
+        // h0-R on are added, so the first removal is at t = h0+1)
+        auto load_step = [&](int64_t t, Stage& p) {
+            const bool rem = t > h0;
+            const auto rCe = row_rsrc(cam, t + R, sizeof(T), true), rCl = row_rsrc(cam, t - R - 1, sizeof(T), rem);
+            const auto rPe = row_rsrc(proj, t + R, sizeof(T), true), rPl = row_rsrc(proj, t - R - 1, sizeof(T), rem);
+            p.ue = ld_buf<T>(rCe, vUe);
+            p.ul = ld_buf<T>(rCl, vUl);
+#pragma unroll
+            for (int j = 0; j < LO; ++j) {
+                if (j > 0 && 64 * j >= NO) break;
+                p.oe[j] = ld_buf<T>(rPe, vO[j]);
+                p.ol[j] = ld_buf<T>(rPl, vO[j]);
+            }
+            const bool st = t >= h0 && t < h1;
+            const auto rPB = row_rsrc(sp.box, t, 8, st), rPS = row_rsrc(sp.sq, t, 4, st);
+            const auto rCB = row_rsrc(sc.box, t, 8, st), rCS = row_rsrc(sc.sq, t, 4, st);
+#pragma unroll
+            for (int j = 0; j < LS; ++j) {
+                if (j > 0 && 64 * j >= NS) break;
+                p.m[j] = ld_buf_f64(rPB, vSd[j]);
+                p.q[j] = ld_buf<float>(rPS, vSf[j]);
+            }
+            p.ub = ld_buf_f64(rCB, vUSd);
+            p.uq = ld_buf<float>(rCS, vUSf);
+        };
+        auto store_step = [&](int b, const Stage& p) {
+            ringU[b * 64 + li] = li < 32 ? (double)p.ue : -(double)p.ul;  // 0 past NX
+#pragma unroll
+            for (int j = 0; j < LO; ++j)
+                if (64 * j < NO && li + 64 * j < NO) {
+                    ringO[(2 * b) * NO + li + 64 * j] = (double)p.oe[j];
+                    ringO[(2 * b + 1) * NO + li + 64 * j] = (double)p.ol[j];
+                }
+#pragma unroll
+            for (int j = 0; j < LS; ++j)
+                if (64 * j < NS && li + 64 * j < NS) {
+                    rsM[b * NS + li + 64 * j] = p.m[j] * rk2;
+                    rsQ[b * NS + li + 64 * j] = p.q[j];
+                }
+            if (li < 16) { usB[b * 16 + li] = -p.ub; usQ[b * 16 + li] = p.uq; }
+        };
+        // three register stages: the loads of step t are issued at step t-3, so two full
+        // steps pass before the loader waits for them (a single step of slack left every
+        // step waiting out a global-load round trip)
+        Stage st[3];
+        load_step(hs, st[0]);
+        store_step(0, st[0]);
+        load_step(hs + 1, st[1]);
+        load_step(hs + 2, st[2]);
+        load_step(hs + 3, st[0]);
+        __syncthreads();
+        // iteration i = t - hs stores step t+1 (stage (i+1)%3) and refills that stage with
+        // step t+4; the barrier count matches the compute waves' exactly
+        auto step = [&](auto kc, int64_t t) {
+            constexpr int k = decltype(kc)::value;  // == (t - hs + 1) % 3
+            const int i = (int)(t - hs);
+            store_step((i + 1) & 1, st[k]);
+            load_step(t + 4, st[k]);  // past the band's end: harmless, unused
+            if constexpr (ARGMAX) {
+                if (t >= h0) __syncthreads();
+            }
+            __syncthreads();
+        };
+        for (int64_t t = hs;; t += 3) {
+            if (t >= h1) break;
+            step(std::integral_constant<int, 1>{}, t);
+            if (t + 1 >= h1) break;
+            step(std::integral_constant<int, 2>{}, t + 1);
+            if (t + 2 >= h1) break;
+            step(std::integral_constant<int, 0>{}, t + 2);
+        }
+        if constexpr (!ARGMAX) __syncthreads();  // the compute waves' final store phase
+        return;
+    }
+
+    // ---- compute waves: lane tid owns diagonal delta = d0 + tid ----
+    const int64_t delta = d0 + tid;
+    int m_lo = TWT, m_hi = 0;  // valid camera-column offsets m in [m_lo, m_hi) (ARGMAX)
     if (delta >= dlo && delta <= dhi) {
         const int64_t lo = max((int64_t)0, -delta - u0);
         const int64_t hi = min((int64_t)TWT, min(g.W - u0 - delta, g.WO - u0));
         m_lo = (int)lo;
         m_hi = (int)max(lo, hi);
     }
-
-    // ---- staging: branch-free raw buffer loads (out-of-range -> 0 = the reference's
-    // zero padding, stereo_matching_kernel.cu:6-12); every lane issues every load, so
-    // the compiler counts outstanding memory operations exactly and never drains the
-    // volume stores (vmcnt(0)) to consume a prefetch ----
-    // per-lane byte offsets inside one row (loop-invariant); the row is the descriptor's base,
-    // and a row outside the image gets a zero-size descriptor (every load returns 0)
-    const int64_t xU0 = u0 - R, xO0 = u0 - R + d0, oS = u0 + d0;
-    constexpr uint32_t OOB = 0x80000000u;
-    auto colOff = [&](bool have, int64_t x, int esz) -> uint32_t {
-        return (have && x >= 0 && x < g.W) ? (uint32_t)(x * esz) : OOB;
-    };
-    const uint32_t vU = colOff(tid < NX, xU0 + tid, sizeof(T));
-    const uint32_t vO0 = colOff(true, xO0 + tid, sizeof(T));
-    const uint32_t vO1 = colOff(tid + NL < NO, xO0 + tid + NL, sizeof(T));
-    const uint32_t vS0d = colOff(true, oS + tid, 8), vS0f = colOff(true, oS + tid, 4);
-    const uint32_t vS1d = colOff(tid + NL < NS, oS + tid + NL, 8), vS1f = colOff(tid + NL < NS, oS + tid + NL, 4);
-    const uint32_t vUSd = colOff(tid < TWT, u0 + tid, 8), vUSf = colOff(tid < TWT, u0 + tid, 4);
-    auto row_rsrc = [&](const void* base, int64_t row, int esz) {
-        const bool ok = row >= 0 && row < g.H;
-        return make_rsrc((const char*)base + (ok ? row : 0) * g.W * esz, ok ? (uint32_t)(g.W * esz) : 0u);
-    };
-    struct Pre {
-        float u, o0, o1, q0, q1, uq;
-        double m0, m1, ub;
-    };
-    auto load_row = [&](int64_t y, Pre& p) {
-        const auto rC = row_rsrc(cam, y, sizeof(T));
-        const auto rP = row_rsrc(proj, y, sizeof(T));
-        p.u = ld_buf<T>(rC, vU);
-        p.o0 = ld_buf<T>(rP, vO0);
-        p.o1 = ld_buf<T>(rP, vO1);
-    };
-    auto load_stats = [&](int64_t h, Pre& p) {
-        const auto rPB = row_rsrc(sp.box, h, 8), rPS = row_rsrc(sp.sq, h, 4);
-        const auto rCB = row_rsrc(sc.box, h, 8), rCS = row_rsrc(sc.sq, h, 4);
-        p.m0 = ld_buf_f64(rPB, vS0d) * rk2;
-        p.q0 = ld_buf<float>(rPS, vS0f);
-        p.m1 = ld_buf_f64(rPB, vS1d) * rk2;
-        p.q1 = ld_buf<float>(rPS, vS1f);
-        p.ub = ld_buf_f64(rCB, vUSd);
-        p.uq = ld_buf<float>(rCS, vUSf);
-    };
-    auto store_row = [&](int slot, const Pre& p) {
-        if (tid < 32) {
-            ringU[slot * 64 + tid] = (double)p.u;        // p.u is 0 for tid >= NX
-            ringU[slot * 64 + 32 + tid] = -(double)p.u;
-        }
-        ringO[slot * NO + tid] = (double)p.o0;
-        if (tid + NL < NO) ringO[slot * NO + tid + NL] = (double)p.o1;
-    };
-    auto store_stats = [&](int b, const Pre& p) {
-        rsM[b * NS + tid] = p.m0;
-        rsQ[b * NS + tid] = p.q0;
-        if (tid + NL < NS) { rsM[b * NS + tid + NL] = p.m1; rsQ[b * NS + tid + NL] = p.q1; }
-        if (tid < 16) { usB[b * 16 + tid] = -p.ub; usQ[b * 16 + tid] = p.uq; }
-    };
-
     double col[NX];
 #pragma unroll
     for (int x = 0; x < NX; ++x) col[x] = 0.0;
     const int r16 = tid & 15;
-    // col[x] += c(row sAdd, x) p(row sAdd, x + delta) - c(row sSub, x) p(row sSub, x + delta).
-    // Operands are loaded in batches of 8 columns ahead of the DPP FMAs (an asm statement
-    // is a scheduling boundary, so loads are not hoisted across it by the compiler).
-    auto update = [&](int sAdd, int sSub) {
-        const double ca0 = ringU[sAdd * 64 + r16], ca1 = ringU[sAdd * 64 + 16 + r16];
-        const double cb0 = ringU[sSub * 64 + 32 + r16], cb1 = ringU[sSub * 64 + 48 + r16];  // negated
-        const double* oa = ringO + sAdd * NO + tid;
-        const double* ob = ringO + sSub * NO + tid;
-        constexpr int B = 8;
-        Unroll<0, (NX + B - 1) / B>::run([&](auto bc) {
-            constexpr int x0 = decltype(bc)::value * B;
+    // col[x] += c(enter, x) p(enter, x + delta) - c(leave, x) p(leave, x + delta)
+    auto update = [&](int b) {
+        const double ca0 = ringU[b * 64 + r16], ca1 = ringU[b * 64 + 16 + r16];
+        const double cb0 = ringU[b * 64 + 32 + r16], cb1 = ringU[b * 64 + 48 + r16];  // negated
+        // volatile: keeps these as single ds_read_b64 (2 LDS cycles per wave-instruction)
+        // instead of pairs merged into ds_read2_b64 (8 cycles, half the bandwidth)
+        const lds_vd* oa = (const lds_vd*)(ringO + (2 * b) * NO + tid);
+        const lds_vd* ob = (const lds_vd*)(ringO + (2 * b + 1) * NO + tid);
+        // batches of B columns, double-buffered: batch b+1's reads are in flight while
+        // batch b's FMAs issue (an asm statement is a scheduling boundary)
+        constexpr int B = 4, NB = (NX + B - 1) / B;
+        double pa[2][B], pb[2][B];
+        auto fetch = [&](auto bc) {
+            constexpr int bb = decltype(bc)::value, x0 = bb * B;
             constexpr int nb = NX - x0 < B ? NX - x0 : B;
-            double pa[B], pb[B];
             Unroll<0, nb>::run([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
-                pa[i] = oa[x0 + i];
-                pb[i] = ob[x0 + i];
+                pa[bb & 1][i] = oa[x0 + i];
+                pb[bb & 1][i] = ob[x0 + i];
             });
+        };
+        fetch(std::integral_constant<int, 0>{});
+        Unroll<0, NB>::run([&](auto bc) {
+            constexpr int bb = decltype(bc)::value, x0 = bb * B;
+            constexpr int nb = NX - x0 < B ? NX - x0 : B;
+            if constexpr (bb + 1 < NB) fetch(std::integral_constant<int, bb + 1>{});
             Unroll<0, nb>::run([&](auto ic) {
                 constexpr int i = decltype(ic)::value, x = x0 + i;
-                fmac_bc64<(x & 15)>(col[x], x < 16 ? ca0 : ca1, pa[i]);
-                fmac_bc64<(x & 15)>(col[x], x < 16 ? cb0 : cb1, pb[i]);
+                fmac_bc64<(x & 15)>(col[x], x < 16 ? ca0 : ca1, pa[bb & 1][i]);
+                fmac_bc64<(x & 15)>(col[x], x < 16 ? cb0 : cb1, pb[bb & 1][i]);
             });
         });
     };
-    // first-step "leaving" row: slot NSLOT-1, all zeros
-    for (int e = tid; e < 64; e += NL) ringU[(NSLOT - 1) * 64 + e] = 0.0;
-    for (int e = tid; e < NO; e += NL) ringO[(NSLOT - 1) * NO + e] = 0.0;
 
-    // ring slot of image row y: (y - (h0 - R)) mod NSLOT, tracked incrementally
-    {
-        Pre p;
-        for (int i = 0; i < K - 1; ++i) {
-            load_row(h0 - R + i, p);
-            store_row(i, p);
-        }
-        load_stats(h0, p);
-        store_stats(0, p);
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int i = 0; i < K - 1; ++i) update(i, NSLOT - 1);
-    int sIn = K - 1, sOut = NSLOT - 1;  // row h+R / row h-R-1 at step h
-    {
-        Pre p;
-        load_row(h0 + R, p);
-        store_row(sIn, p);
-    }
-    __syncthreads();
-
-    // volume stores: per step one descriptor at the first volume element of the tile's
-    // rows; per lane byte offset m*stride + column (out-of-range for invalid voxels)
-    const int64_t stride = g.layout == CUSTMA_LAYOUT_WINDOW ? g.DO : g.DO + 1;
-    const int64_t lane0 = g.layout == CUSTMA_LAYOUT_WINDOW ? delta : u0 + delta;  // column index at m = 0
-    const int64_t orow = g.WO * g.DO;
+    // ---- store phase: the previous step's staged tile, written so that every 64-byte
+    // sector of the volume is covered by one store instruction of one workgroup.  Row m
+    // of the tile, chunk c: owned columns [cb, cb + len) (sweep.h), lane tid stores column
+    // cb + tid; a per-row descriptor of len columns drops the lanes past the range ----
+    const int DO = (int)g.DO;
+    auto bound = [&](int c, int beta) -> int {  // first owned column of chunk c in a row
+        if (c <= 0) return 0;
+        if (c >= sg.nChunk) return DO;
+        const int x = c * sg.S;
+        return min(DO, x + ((16 - ((beta + x) & 15)) & 15));
+    };
+    // Sector phase of each volume row of the tile: the same for every row band step when
+    // WO*DO is a multiple of 16 (then computed once); otherwise the chunks split at c*S
+    // (S is a multiple of 16) -- still a partition, only not sector aligned.
+    // Per lane and tile row m: byte offset of its volume element inside the row tile
+    // (out of range for lanes past the owned columns); the staging slot of that element
+    // is the same offset plus a per-row constant.
     uint32_t voff[TWT];
+    {
+        const bool phase_fixed = ((g.WO * g.DO) & 15) == 0;
+        const int r0 = (int)((((h0 - g.h_lo) * g.WO + u0)) & 15), dm = phase_fixed ? DO & 15 : 0;
 #pragma unroll
-    for (int m = 0; m < TWT; ++m)
-        voff[m] = (m >= m_lo && m < m_hi) ? (uint32_t)((m * stride + lane0) * 4) : 0x80000000u;
-    float* obase = out + ((h0 - g.h_lo) * g.WO + u0) * g.DO;
+        for (int m = 0; m < TWT; ++m) {
+            const int beta = ((r0 + m) * dm) & 15;
+            const int cb = bound(chunk, beta), ce = bound(chunk + 1, beta);
+            const bool ok = u0 + m < g.WO && cb + tid < ce;
+            voff[m] = ok ? (uint32_t)((m * DO + cb + tid) * 4) : OOB;
+        }
+    }
+    // staging index of column c in row m: m*NL + c - d0 - (u0 + m) (full) / m*NL + c - d0
+    // (window); with c = voff/4 - m*DO that is voff/4 + m*stgA + stgB
+    const int stgA = NL - DO - (window ? 0 : 1), stgB = -(int)d0 - (window ? 0 : (int)u0);
+    auto store_tile = [&](int64_t h, int b) {
+        const auto rOut = make_rsrc(out + ((h - g.h_lo) * g.WO + u0) * g.DO, 0x7FFFFFF0u);
+        const char* tile = (const char*)(stg + b * 16 * NL);
+        float v[TWT];
+#pragma unroll
+        for (int m = 0; m < TWT; ++m) v[m] = *(const float*)(tile + voff[m] + 4 * (m * stgA + stgB));
+#ifndef CUSTMA_ABL_NOSTORE  // ablation builds only (scripts/build_ablations.py)
+#pragma unroll
+        for (int m = 0; m < TWT; ++m) st_buf(v[m], rOut, voff[m]);
+#else
+#pragma unroll
+        for (int m = 0; m < TWT; ++m)
+            if (v[m] == 1234.5f) st_buf(v[m], rOut, voff[m]);
+#endif
+    };
 
-    for (int64_t h = h0; h < h1; ++h) {
-        const int buf = (int)((h - h0) & 1);
-        Pre p;  // next row (harmless loads past the band's end: results unused)
-        load_row(h + R + 1, p);
-        load_stats(h + 1, p);
-        update(sIn, sOut);
-
-        double s = 0.0;
+    __syncthreads();  // the loader's first stage
+    for (int64_t h = hs; h < h1; ++h) {
+        const int buf = (int)((h - hs) & 1);
+        if constexpr (!ARGMAX) {
+            if (h > h0) store_tile(h - 1, buf ^ 1);
+        }
+#ifndef CUSTMA_ABL_NOUPDATE  // ablation builds only (scripts/build_ablations.py)
+        update(buf);
+#endif
+#ifdef CUSTMA_ABL_NOOUT
+        if (h >= h0 && ARGMAX) {
+#else
+        if (h >= h0) {
+#endif
+            double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
 #pragma unroll
-        for (int x = 0; x < 2 * R + 1; ++x) s += col[x];
-        const double* mrow = rsM + buf * NS + tid;
-        const float* qrow = rsQ + buf * NS + tid;
-        const double nb = usB[buf * 16 + r16];  // -(camera patch sum) of column r16
-        const float uq = usQ[buf * 16 + r16];   // camera ex2 of column r16
-        double mv[TWT];
-        float qv[TWT];
+            for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
+            const lds_vd* mrow = (const lds_vd*)(rsM + buf * NS + tid);
+            const float* qrow = rsQ + buf * NS + tid;
+            const double nb = usB[buf * 16 + r16];  // -(camera patch sum) of column r16
+            const float uq = usQ[buf * 16 + r16];   // camera ex2 of column r16
+            double mv[TWT];
+            float qv[TWT];
 #pragma unroll
-        for (int m = 0; m < TWT; ++m) { mv[m] = mrow[m]; qv[m] = qrow[m]; }
-        const auto rOut = make_rsrc(ARGMAX ? (float*)nullptr : obase, 0x7FFFFFF0u);
-        Unroll<0, TWT>::run([&](auto mc) {
-            constexpr int m = decltype(mc)::value;
-            if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
-            double e = s;
-            fmac_bc64<m>(e, nb, mv[m]);                 // E = S - box_c * mean_p
-            float den2 = kEps;
-            fmac_bc32<m>(den2, uq, qv[m]);              // ex2 * ey2 + eps
-            const float num = (float)e + kEps;
-            const float c = num * __builtin_amdgcn_rsqf(den2);
-            if constexpr (ARGMAX) {
-                red[m * NL + tid] = (m >= m_lo && m < m_hi) ? c : -FLT_MAX;
-            } else {
-                st_buf(c, rOut, voff[m]);
-            }
-        });
-        if constexpr (!ARGMAX) obase += orow;
-        if constexpr (ARGMAX) {
-            __syncthreads();
-            // TPR threads per camera column (power of two), PER diagonals each, in order
-            int TPR = 1;
-            while (TPR * 2 * TWT <= NL && TPR < 16) TPR *= 2;
-            const int PER = (NL + TPR - 1) / TPR;
-            const int m = tid / TPR, part_i = tid % TPR;
-            const bool red_live = m < TWT;
-            float best = -FLT_MAX, second = -FLT_MAX;
-            int bi = 0x7fffffff;
-            for (int e = 0; red_live && e < PER; ++e) {
-                const int l = part_i * PER + e;
-                if (l >= NL) break;
-                const float v = red[m * NL + l];
-                if (v > best) { second = best; best = v; bi = l; }
-                else if (v > second) second = v;
-            }
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) {
-                if (off >= TPR) break;
-                const float ob = __shfl_xor(best, off), os = __shfl_xor(second, off);
-                const int oi = __shfl_xor(bi, off);
-                if (ob > best || (ob == best && oi < bi)) {
-                    second = fmaxf(os, best); best = ob; bi = oi;
+            for (int m = 0; m < TWT; ++m) { mv[m] = mrow[m]; qv[m] = qrow[m]; }
+            float* srow = stg + (ARGMAX ? 0 : buf * 16 * NL) + tid;
+            Unroll<0, TWT>::run([&](auto mc) {
+                constexpr int m = decltype(mc)::value;
+                if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
+                double e = s;
+                fmac_bc64<m>(e, nb, mv[m]);                 // E + eps = S + eps - box_c * mean_p
+                float den2 = kEps;
+                fmac_bc32<m>(den2, uq, qv[m]);              // ex2 * ey2 + eps
+                const float c = (float)e * __builtin_amdgcn_rsqf(den2);
+                if constexpr (ARGMAX) {
+                    srow[m * NL] = (m >= m_lo && m < m_hi) ? c : -FLT_MAX;
                 } else {
-                    second = fmaxf(second, ob);
+                    srow[m * NL] = c;
                 }
-            }
-            const int64_t u = u0 + m;
-            if (red_live && part_i == 0 && u < g.WO) {
-                const int64_t pidx = ((int64_t)chunk * g.HV() + (h - g.h_lo)) * g.WO + u;
-                part.best[pidx] = best;
-                part.second[pidx] = second;
-                int64_t sidx = -1;
-                if (best > -FLT_MAX) {
-                    const int64_t dd = d0 + bi;
-                    sidx = g.layout == CUSTMA_LAYOUT_WINDOW ? dd : u + dd;
+            });
+            if constexpr (ARGMAX) {
+                __syncthreads();
+                // TPR threads per camera column (power of two), PER diagonals each, in order
+                int TPR = 1;
+                while (TPR * 2 * TWT <= NL && TPR < 16) TPR *= 2;
+                const int PER = (NL + TPR - 1) / TPR;
+                const int m = tid / TPR, part_i = tid % TPR;
+                const bool red_live = m < TWT;
+                float best = -FLT_MAX, second = -FLT_MAX;
+                int bi = 0x7fffffff;
+                for (int e = 0; red_live && e < PER; ++e) {
+                    const int l = part_i * PER + e;
+                    if (l >= NL) break;
+                    const float v = stg[m * NL + l];
+                    if (v > best) { second = best; best = v; bi = l; }
+                    else if (v > second) second = v;
                 }
-                part.index[pidx] = (int32_t)sidx;
+                for (int off = 1; off < TPR; off <<= 1) {
+                    const float ob = __shfl_xor(best, off), os = __shfl_xor(second, off);
+                    const int oi = __shfl_xor(bi, off);
+                    if (ob > best || (ob == best && oi < bi)) {
+                        second = fmaxf(os, best); best = ob; bi = oi;
+                    } else {
+                        second = fmaxf(second, ob);
+                    }
+                }
+                const int64_t u = u0 + m;
+                if (red_live && part_i == 0 && u < g.WO) {
+                    const int64_t pidx = ((int64_t)chunk * g.HV() + (h - g.h_lo)) * g.WO + u;
+                    part.best[pidx] = best;
+                    part.second[pidx] = second;
+                    int64_t sidx = -1;
+                    if (best > -FLT_MAX) {
+                        const int64_t dd = d0 + bi;
+                        sidx = window ? dd : u + dd;
+                    }
+                    part.index[pidx] = (int32_t)sidx;
+                }
             }
         }
-        // next step: row h+R+1 enters (into the slot after sIn), row h-R leaves
-        sOut = sIn + 1 - K >= 0 ? sIn + 1 - K : sIn + 3;  // slot of row h-R = (sIn - 2R) mod (K+2)
-        sIn = sIn + 1 == NSLOT ? 0 : sIn + 1;
-        store_row(sIn, p);
-        store_stats(buf ^ 1, p);
+        __syncthreads();
+    }
+    if constexpr (!ARGMAX) {
+        if (h1 > h0) store_tile(h1 - 1, (int)((h1 - 1 - hs) & 1));
         __syncthreads();
     }
 }
@@ -316,18 +397,18 @@ __global__ __launch_bounds__(320, 2) void k_sweep_fwd(const T* __restrict__ cam,
 template <int K, typename T>
 hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out,
                     DispPartial* part, hipStream_t s) {
-    const SweepGrid sg = sweep_grid(g);
-    constexpr int R = K / 2, NX = TW + 2 * R, NSLOT = K + 2;
+    const SweepGrid sg = sweep_grid(g, /*owned=*/part == nullptr);
+    constexpr int R = K / 2, NX = TW + 2 * R;
     const int NL = sg.NL, NO = NX + NL - 1, NS = TW + NL - 1;
-    size_t lds = sizeof(double) * (2 * NS + 2 * 16 + NSLOT * 64 + NSLOT * NO) + sizeof(float) * (2 * NS + 2 * 16);
+    const size_t lds = sizeof(double) * (4 * NO + 2 * 64 + 2 * NS + 2 * 16) +
+                       sizeof(float) * (2 * NS + 2 * 16 + (part ? 1 : 2) * TW * NL);
     const int64_t blocks = sweep_blocks(sg);
     if (part) {
-        lds += sizeof(float) * TW * NL;
-        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true>), dim3((unsigned)blocks), dim3(NL), lds, s, cam, proj, g,
+        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam, proj, g,
                            sc, sp, out, sg, *part);
     } else {
         DispPartial none{};
-        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false>), dim3((unsigned)blocks), dim3(NL), lds, s, cam, proj, g,
+        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam, proj, g,
                            sc, sp, out, sg, none);
     }
     return hipGetLastError();

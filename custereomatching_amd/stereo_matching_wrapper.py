@@ -102,10 +102,12 @@ def _rows(H: int, rows: Optional[Tuple[int, int]]) -> Tuple[int, int]:
 
 def cost_volume_forward(camera: torch.Tensor, projector: torch.Tensor, D: int, kernel_size: int,
                         layout: str = "full", precision: Optional[str] = None,
-                        rows: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+                        rows: Optional[Tuple[int, int]] = None,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Forward volume without autograd (reference: stereo::stereo_matching_forward,
     custma/src/stereo_matching.cpp:16-42).  ``rows=(b, e)`` computes only volume
-    rows [b, e) of a haloed row band (custma_forward_band)."""
+    rows [b, e) of a haloed row band (custma_forward_band).  ``out`` is an optional
+    preallocated contiguous float32 volume on the images' device."""
     code = _check_pair(camera, projector, kernel_size)
     lay = _LAYOUTS[layout]
     prec = _PRECISIONS[precision or default_precision()]
@@ -115,7 +117,11 @@ def cost_volume_forward(camera: torch.Tensor, projector: torch.Tensor, D: int, k
     Dl = D if lay == _lib.LAYOUT_WINDOW else 0
     WO, DO = _lib.volume_dims(H, W, lay, Dl)
     dev = camera.device
-    out = torch.empty((r1 - r0, WO, DO), dtype=torch.float32, device=dev)
+    if out is None:
+        out = torch.empty((r1 - r0, WO, DO), dtype=torch.float32, device=dev)
+    elif (tuple(out.shape) != (r1 - r0, WO, DO) or out.dtype != torch.float32 or out.device != dev
+          or not out.is_contiguous()):
+        raise ValueError(f"out must be a contiguous float32 tensor of shape {(r1 - r0, WO, DO)} on {dev}")
     if out.numel() == 0:
         return out
     with torch.cuda.device(dev):

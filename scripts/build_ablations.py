@@ -1,0 +1,13 @@
+"""Build ablation variants of the HIP library into scripts/_abl/<name>/ (git-ignored)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from custereomatching_amd.build import build_variant
+HERE = os.path.dirname(os.path.abspath(__file__))
+VARIANTS = {"nostore": ["CUSTMA_ABL_NOSTORE"], "noupdate": ["CUSTMA_ABL_NOUPDATE"],
+            "nothing": ["CUSTMA_ABL_NOSTORE", "CUSTMA_ABL_NOUPDATE"],
+            "storeonly": ["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT"], "skeleton": ["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT", "CUSTMA_ABL_NOSTORE"],
+            "aux1": ["CUSTMA_STORE_AUX=1"], "aux2": ["CUSTMA_STORE_AUX=2"], "aux16": ["CUSTMA_STORE_AUX=16"],
+            "aux3": ["CUSTMA_STORE_AUX=3"], "aux17": ["CUSTMA_STORE_AUX=17"], "aux18": ["CUSTMA_STORE_AUX=18"],
+            "aux19": ["CUSTMA_STORE_AUX=19"]}
+for n in (sys.argv[1:] or VARIANTS):
+    print(build_variant(os.path.join(HERE, "_abl", n), VARIANTS[n]))

@@ -22,7 +22,7 @@ def run(name, ops, reps):
             out = cm.cost_volume_forward(cam, proj, D, k, lay, prec)
             et = EventTimer()
             for _ in range(reps):
-                et.record(lambda: cm.cost_volume_forward(cam, proj, D, k, lay, prec, ))
+                et.record(lambda: cm.cost_volume_forward(cam, proj, D, k, lay, prec, out=out))
             ms = et.mean_ms()
             nb = out.numel() * 4 + 2 * H * W * cam.element_size()
             res[f"fwd_{prec}_ms"] = round(ms, 4)
