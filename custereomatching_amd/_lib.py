@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("CUSTMA_LIB") or os.path.join(_HERE, "_lib", "libcustm
 F32, F16 = 0, 1
 LAYOUT_FULL, LAYOUT_WINDOW = 0, 1
 EXACT, FAST = 0, 1
-OP_FORWARD, OP_BACKWARD, OP_DISPARITY = 0, 1, 2
+OP_FORWARD, OP_BACKWARD, OP_DISPARITY, OP_BACKWARD_RECOMPUTE = 0, 1, 2, 3
 E_ARG, E_NULL, E_WORKSPACE, E_LAUNCH, E_UNSUPPORTED = -1, -2, -3, -4, -5
 
 EXPORTS = ("custma_abi_version", "custma_last_error", "custma_volume_dims", "custma_workspace_bytes",
@@ -43,11 +43,12 @@ def _load():
     lib.custma_workspace_bytes.argtypes = [i64, i64, i32, i32, i32, i32]
     lib.custma_workspace_bytes.restype = sz
     lib.custma_forward.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i32, vp, vp, sz, vp]
-    lib.custma_backward.argtypes = [vp, vp, vp, i32, i64, i64, i32, i32, i32, vp, vp, vp, sz, vp]
+    lib.custma_backward.argtypes = [vp, vp, vp, vp, i32, i64, i64, i32, i32, i32, vp, vp, vp, sz, vp]
     lib.custma_argmax.argtypes = [vp, i64, i64, vp, vp, vp]
     lib.custma_disparity.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, vp, vp, vp, vp, sz, vp]
     lib.custma_forward_band.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i32, i64, i64, vp, vp, sz, vp]
-    lib.custma_backward_band.argtypes = [vp, vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, vp, vp, vp, sz, vp]
+    lib.custma_backward_band.argtypes = [vp, vp, vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, vp, vp, vp, sz,
+                                         vp]
     lib.custma_disparity_band.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, vp, vp, vp, vp, sz,
                                           vp]
     for name in ("custma_forward", "custma_backward", "custma_argmax", "custma_disparity",

@@ -1,0 +1,706 @@
+// Backward: gradients of sum(grad * volume) w.r.t. both images in ONE pass
+// over the incoming gradient volume (deterministic, no atomics).
+//
+// The reference (custma/src/stereo_matching_kernel.cu:75-179) forms, per
+// voxel and tap t, g * (y_t / S - Y x_t (E+eps) / S^3) and scatters it with
+// float atomics (k^2 recomputed taps + k^2 atomics per voxel).  Summed over
+// voxels, with A = g / S and V = g (E+eps) / S^3 = A * cost / S (`cost` = the
+// forward's output), the gradients split into per-diagonal box sums:
+//
+//   dC(y,x) = T1c(y,x) - Box[Am](y,x) - c'(y,x) Box[B](y,x)  + Box[mc' B](y,x)
+//   dP(y,o) = T1p(y,o) - Box[Ac](y,o) - p'(y,o) Box[Bp](y,o) + Box[mp' Bp](y,o)
+//
+//   BoxA(y,x,dl) = sum of A(h,w,dl) over |h-y|,|w-x| <= r     (fixed diagonal dl = d - w)
+//   T1c(y,x) = sum_dl p'(y,x+dl) BoxA(y,x,dl)      T1p(y,o) = sum_dl c'(y,o-dl) BoxA(y,o-dl,dl)
+//   Am(h,w)  = sum_dl A mp'(h,w+dl)   B(h,w)  = sum_dl V Y(h,w+dl)
+//   Ac(h,o)  = sum_w  A mc'(h,w)      Bp(h,o) = sum_w  V X(h,w)
+//
+// X, Y are the centred second moments of the camera / projector patches, m
+// their means, and c' = c - cbar, p' = p - pbar (zero padding included, so an
+// out-of-image tap is -cbar): the gradient is exactly invariant under a
+// global shift of either image, and shifting by the image mean removes the
+// cancellation between T1 and Box[Am] (and between c Box[B] and Box[mc B])
+// that otherwise makes fp32 accumulation lose ~1e-5 of the result on smooth
+// images.  With the shift every sum here is fp32 (validated against the fp64
+// oracle on textured, smooth, quantised and all-ones inputs).
+//
+// Sweep layout ("column sweep"): one wave = 64 consecutive diagonals (lane
+// l owns dl = d0 + l) x 16 image rows (registers), walking the camera
+// columns w.  Per step it loads the gradient row segment g[h][w][w+dl] of
+// NY = 16 + 2r rows (256 contiguous bytes per row), forms A, keeps the
+// horizontal sliding sums HA[y] of A (NY registers, the leaving column's A
+// recomputed from its gradient -- an L2/MALL re-read), and the vertical box
+// over the registers gives BoxA for its 16 own rows.  Camera-side values of
+// one step belong to one camera pixel per row and are summed across the
+// lanes (permlane32/16 swaps + DPP butterflies, 106 VALU for 48 sums);
+// projector-side values of lane l belong to projector column w + dl + const,
+// which moves down one lane per step, so they accumulate in registers with a
+// DPP wave_shl:1 fused into the add, and lane 0's completed column is
+// emitted every step.  Both go through a 16-step LDS buffer to coalesced
+// stores of fp32 partial sums per diagonal chunk; k_bwd_gather sums the
+// chunks and k_bwd_combine applies the box filters.
+#include "common.h"
+#include "sweep.h"
+#include "xlane.h"
+
+namespace custma {
+
+namespace {
+
+constexpr int TRB = 16;   // own rows per wave
+constexpr int NLB = 64;   // diagonals per wave
+constexpr int FB = 16;    // steps per flush
+constexpr int NTYPE = 6;  // partial types: T1c, Am, B (camera) | T1p, Ac, Bp (projector)
+constexpr int kRGT = 4;   // row groups per XCD tile
+constexpr int kSeg = 128; // pixel columns per wave (>= 64 + 2 r: segments s and s+2 never overlap)
+constexpr uint32_t kOOB = 0x80000000u;
+
+// Chunk geometry (host and device): diagonals [d0, d0+64); camera columns that carry
+// a valid voxel for some lane: [wlo, whi); pixel columns whose box touches one:
+// [wlo - r, whi + r), cut into segments of kSeg columns (one wave each).
+struct ChunkGeo {
+    int64_t d0, wlo, whi;
+};
+__host__ __device__ inline ChunkGeo chunk_geo(const Geo& g, int64_t dlo, int j) {
+    ChunkGeo c;
+    c.d0 = dlo + (int64_t)NLB * j;
+    if (g.layout == CUSTMA_LAYOUT_WINDOW) {
+        c.wlo = 0;
+        c.whi = g.WO;
+    } else {
+        const int64_t a = -(c.d0 + NLB - 1);
+        c.wlo = a > 0 ? a : 0;
+        const int64_t b = g.W - c.d0;
+        c.whi = b < g.W ? b : g.W;
+    }
+    return c;
+}
+__host__ __device__ inline int chunk_nseg(const ChunkGeo& c, int r) {
+    return (int)((c.whi - c.wlo + 2 * r + kSeg - 1) / kSeg);
+}
+// Segment s of chunk c: output pixel columns [xs, xe); the sweep runs w in [xs - r, xe + r).
+__host__ __device__ inline void seg_cols(const ChunkGeo& c, int r, int s, int64_t* xs, int64_t* xe) {
+    const int64_t tlo = c.wlo - r, thi = c.whi + r;
+    *xs = tlo + (int64_t)s * kSeg;
+    const int64_t e = *xs + kSeg;
+    *xe = e < thi ? e : thi;
+}
+// Written column range [lo, hi) of partial type t for segment s of chunk c (before clipping
+// to [0, W)).  Camera types: the segment's own columns.  Projector types: every column
+// whose accumulator passed lane 0 during the sweep or sat in the wave at its end.
+__host__ __device__ inline void seg_range(const ChunkGeo& c, int r, int s, int t, int64_t* lo, int64_t* hi) {
+    int64_t xs, xe;
+    seg_cols(c, r, s, &xs, &xe);
+    const int64_t w0 = xs - r, w1 = xe + r;  // sweep steps [w0, w1)
+    switch (t) {
+        case 0: case 1: case 2: *lo = xs; *hi = xe; break;                                // T1c, Am, B
+        case 3: *lo = w0 - 1 - r + c.d0; *hi = w1 - 1 - r + c.d0 + NLB; break;              // T1p
+        default: *lo = w0 - 1 + c.d0; *hi = w1 - 1 + c.d0 + NLB; break;                     // Ac, Bp
+    }
+}
+// Union over the chunk's segments (contiguous).
+__host__ __device__ inline void type_range(const ChunkGeo& c, int r, int t, int64_t* lo, int64_t* hi) {
+    int64_t l0, h0, l1, h1;
+    seg_range(c, r, 0, t, &l0, &h0);
+    seg_range(c, r, chunk_nseg(c, r) - 1, t, &l1, &h1);
+    *lo = l0;
+    *hi = h1;
+}
+
+struct BwdArgs {
+    const void* cam;
+    const void* proj;
+    Stats sc, sp;
+    // prepared fp32 images [H][W] (k_bwd_prep): camera X, mc', c and projector Y, mp', p
+    const float *Xc, *mcc, *cc, *Yp, *mpp, *pp;
+    const float* grad;
+    const float* vol;
+    const float* shift;  // [2]: cbar, pbar
+    float* part;         // [NTYPE][S][H][W]
+    const int* cover;    // [4][2][W]: first chunk, count per (range class, column)
+    int S, Sj, nChunk, nRG, jc, nsegMax;
+    int64_t dlo, ylo, yhi;
+};
+
+__device__ __forceinline__ int chunk_of_rank(int r, int n, int jc) {
+    // longest chunks (diagonals near 0 in the full layout) first: jc, jc+1, jc-1, ...
+    const int below = jc, above = n - 1 - jc, m = below < above ? below : above;
+    if (r <= 2 * m) {
+        if (r == 0) return jc;
+        const int s = (r + 1) / 2;
+        return (r & 1) ? jc + s : jc - s;
+    }
+    const int rest = r - 2 * m;
+    return above > below ? jc + m + rest : jc - m - rest;
+}
+
+template <int K>
+__device__ __forceinline__ void bwd_sweep_body(const Geo& g, const BwdArgs& a, int j, int sg, int rg,
+                                               float (*cbuf)[48], float (*pbuf)[48]) {
+    constexpr int R = K / 2, NY = TRB + 2 * R;
+    static_assert(NY <= 32, "two row-replicated registers cover the rows");
+
+    const ChunkGeo cg = chunk_geo(g, a.dlo, j);
+    const int lane = threadIdx.x;
+    // lane-level index math in 32 bits (images and one volume row slab < 2 GiB: backward_supported)
+    const int Wi = (int)g.W, Hi = (int)g.H;
+    const int d0 = (int)cg.d0, dl = d0 + lane;
+    const int64_t y0 = a.ylo + (int64_t)TRB * rg;
+    const int y0i = (int)y0;
+    int64_t xs64, xe64;  // output pixel columns of this segment; sweep steps w in [w0, wend)
+    seg_cols(cg, R, sg, &xs64, &xe64);
+    const int xs = (int)xs64, xe = (int)xe64;
+    const int w0 = xs - R, wend = xe + R;
+    const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
+    // this lane's voxel columns [lwlo, lwhi)
+    int lwlo, lwhi;
+    if (window) {
+        lwlo = 0;
+        lwhi = (dl >= 0 && dl <= g.D) ? (int)g.WO : 0;
+    } else {
+        lwlo = dl < 0 ? -dl : 0;
+        lwhi = min((int)g.WO, Wi - dl);
+    }
+    const int gsU = (int)g.DO + (window ? 0 : 1);
+    const int slot = 2 * (j % a.Sj) + (sg & 1);
+    const size_t plane = (size_t)g.H * g.W;
+    const float cb = a.shift[0], pb = a.shift[1];
+
+    // Descriptors: whole fp32 images (< 2 GiB, checked on the host) and the volume from the
+    // wave's first volume row; rows are selected with a wave-uniform soffset, columns and
+    // lane validity with the per-lane voffset (0x80000000 = out of range = 0).
+    const uint32_t ib = (uint32_t)(plane * 4);
+    const auto rXc = make_rsrc(a.Xc, ib), rMc = make_rsrc(a.mcc, ib), rCc = make_rsrc(a.cc, ib);
+    const auto rYp = make_rsrc(a.Yp, ib), rMp = make_rsrc(a.mpp, ib), rPp = make_rsrc(a.pp, ib);
+    const size_t slab = (size_t)g.WO * g.DO;  // volume floats per row
+    const int64_t vrow0 = max(g.h_lo, y0 - R);  // first volume row this wave reads
+    const auto rG = make_rsrc(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
+    const auto rV = make_rsrc(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
+    // (voffset + soffset stays below 0x7FFFFFF0 for in-volume rows: backward_supported)
+
+    // soffset of row y0 - R + y: image rows clamped into the image (values of clamped rows
+    // only ever multiply a zero gradient or feed outputs that are not stored), volume rows
+    // relative to vrow0 (rows outside the volume only in EDGE waves, where they are masked)
+    const int64_t ir0 = y0 - R;
+    const uint32_t vstride = (uint32_t)(slab * 4);
+    const int hlo = (int)g.h_lo, hhi = (int)g.h_hi, vrow0i = (int)vrow0;
+    auto img_off = [&](int row, int col) -> uint32_t {
+        return (row >= 0 && row < Hi && col >= 0 && col < Wi) ? (uint32_t)((row * Wi + col) * 4) : kOOB;
+    };
+    auto col_off = [&](int col) -> uint32_t { return (col >= 0 && col < Wi) ? (uint32_t)(col * 4) : kOOB; };
+
+    float HA[NY];
+#pragma unroll
+    for (int y = 0; y < NY; ++y) HA[y] = 0.f;
+    float P[3][TRB];  // projector accumulators: T1p, Ac, Bp
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int m = 0; m < TRB; ++m) P[t][m] = 0.f;
+
+    const int m16 = lane & 15;
+    // Partial planes of this wave: type t, slot, rows [y0, y0 + 16) (rows past yhi out of range)
+    const uint32_t prow_bytes = (uint32_t)(min((int64_t)TRB, a.yhi - y0) * g.W * 4);
+    auto part_rsrc = [&](int t) {
+        return make_rsrc(a.part + ((size_t)t * a.S + slot) * plane + (size_t)y0 * g.W, prow_bytes);
+    };
+    auto flush = [&](int wfirst, int nsteps) {
+        // pair p = type*16 + m; step jcol of the buffer = column wfirst + jcol.  The lane
+        // index is made opaque so the per-lane store offsets are formed here, not hoisted
+        // out of the sweep (they would pin ~50 VGPRs).
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int jcol = ln & 15, pg = ln >> 4;
+        const bool live = jcol < nsteps;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            const int t = i >> 2, p = pg + 4 * i, m = p & 15;  // t is uniform per i
+            const int col = wfirst + jcol - (t == 0 ? R : 0);
+            const bool cok = live && col >= xs && col < xe && col >= 0 && col < Wi;
+            const uint32_t off = cok ? (uint32_t)((m * Wi + col) * 4) : kOOB;
+            st_buf(cbuf[jcol][p], part_rsrc(t), off);
+            // projector saves: column (w - 1 + off + d0) for the step at w
+            const int pcol = wfirst + jcol - 1 + (t == 0 ? -R : 0) + d0;
+            const uint32_t poff = (live && pcol >= 0 && pcol < Wi) ? (uint32_t)((m * Wi + pcol) * 4) : kOOB;
+            st_buf(pbuf[jcol][p], part_rsrc(3 + t), poff);
+        }
+    };
+
+    // Camera-side sums: pairs are folded across lanes as soon as both members exist
+    // (am,b of one row: permlane32; two rows: permlane16; T1c rows likewise), so at most
+    // 12 partly reduced registers are live; reduce_tail12 finishes them.  Which of the 48
+    // sums (type*16 + row) a lane ends up with is found once by running the same tree on
+    // the sums' indices placed in lane 0.
+    float wA[12];
+    auto cam_reduce = [&](auto&& am, auto&& b, auto&& t1) -> float {
+        Unroll<0, TRB / 2>::run([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            wA[i] = red16(red32(am(2 * i), b(2 * i)), red32(am(2 * i + 1), b(2 * i + 1)));
+        });
+        Unroll<0, TRB / 4>::run([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            wA[8 + i] = red16(red32(t1(4 * i), t1(4 * i + 1)), red32(t1(4 * i + 2), t1(4 * i + 3)));
+        });
+        return reduce_tail12(wA, lane);
+    };
+    int qlane;
+    {
+        const bool l0 = lane == 0;
+        qlane = (int)cam_reduce([&](int m) { return l0 ? (float)(16 + m) : 0.f; },
+                                [&](int m) { return l0 ? (float)(32 + m) : 0.f; },
+                                [&](int m) { return l0 ? (float)m : 0.f; });
+    }
+
+    for (int wfirst = w0; wfirst < wend; wfirst += FB) {
+    const int nsteps = min(FB, wend - wfirst);
+#pragma unroll 1
+    for (int s = 0; s < nsteps; ++s) {
+        const int w = wfirst + s;
+        // ---- emit lane 0 of the projector accumulators (their completed column)
+        if (lane == 0) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+                for (int m = 0; m < TRB; m += 4)
+                    *(float4*)&pbuf[s][t * 16 + m] = make_float4(P[t][m], P[t][m + 1], P[t][m + 2], P[t][m + 3]);
+        }
+        const int xb = w - R;  // pixel column whose box is complete this step
+        const int wl = w - K;  // column leaving the horizontal window
+        // the leaving column was added only if it is a step of this sweep
+        const bool ve = w >= lwlo && w < lwhi, vl = wl >= lwlo && wl < lwhi && wl >= w0;
+        // contributions of this segment only: T1 for pixel columns in [xs, xe) (the first
+        // 2r steps only fill the box), per-voxel terms for camera columns in [xs, xe)
+        const float tf = xb >= xs ? 1.f : 0.f, af = (w >= xs && w < xe) ? 1.f : 0.f;
+        const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
+        const uint32_t oGl = vl ? (uint32_t)((wl * gsU + dl) * 4) : kOOB;
+        const uint32_t oYe = col_off(w + dl), oYl = col_off(wl + dl), oPq = col_off(xb + dl);
+        // row-replicated per-row values (lane i: row y = 16 h + (i & 15) of the NY rows)
+        float xe[2], xl[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = (int)ir0 + 16 * h + m16;
+            const bool rok = 16 * h + m16 < NY;
+            xe[h] = ld_buf<float>(rXc, rok ? img_off(row, w) : kOOB);
+            xl[h] = ld_buf<float>(rXc, rok ? img_off(row, wl) : kOOB);
+        }
+        // own rows: mc'(y0+m, w), c'(y0+m, xb)
+        const float mco = ld_buf<float>(rMc, img_off(y0i + m16, w)) * af;
+        const float cxo = (ld_buf<float>(rCc, img_off(y0i + m16, xb)) - cb) * tf;
+        // Row offsets, rebuilt every step (keeps them out of the loop-invariant SGPR set).
+        // Image rows are clamped into the image (a clamped row's values only multiply a zero
+        // gradient or feed outputs that are not stored).  The range check includes soffset
+        // (gfx950, scripts/micro/soffset_test.hip): a row outside the volume gets an soffset
+        // past the descriptor's end and reads zeros.
+        int ir = (int)ir0;
+        asm volatile("" : "+s"(ir));
+        auto iso = [&](int y) -> uint32_t {
+            int rr = ir + y;
+            rr = rr < 0 ? 0 : rr >= Hi ? Hi - 1 : rr;
+            return (uint32_t)rr * (uint32_t)(Wi * 4);
+        };
+        auto vso = [&](int y) -> uint32_t {
+            const int row = ir + y;
+            return (row >= hlo && row < hhi) ? (uint32_t)(row - vrow0i) * vstride : 0x7FFFFFF0u;
+        };
+
+        // ---- A entering (column w) and leaving (column w - k) on the NY rows; the loads of
+        // row y + 2 are issued before row y is computed (sched barriers keep that order and
+        // stop the scheduler from hoisting all rows' loads, which would pin ~150 VGPRs)
+        struct RowLd {
+            float ge, gl, Ye, Yl, cv, mp;
+        };
+        RowLd rl[NY];
+        auto issue = [&](auto yc) {
+            constexpr int y = decltype(yc)::value;
+            const uint32_t so = vso(y), sy = iso(y);
+            rl[y].ge = ld_bufs<float>(rG, oGe, so);
+            rl[y].gl = ld_bufs<float>(rG, oGl, so);
+            rl[y].Ye = ld_bufs<float>(rYp, oYe, sy);
+            rl[y].Yl = ld_bufs<float>(rYp, oYl, sy);
+            if constexpr (y >= R && y < R + TRB) {
+                rl[y].cv = ld_bufs<float>(rV, oGe, so);
+                rl[y].mp = ld_bufs<float>(rMp, oYe, sy);
+            }
+        };
+        issue(std::integral_constant<int, 0>{});
+        if constexpr (NY > 1) issue(std::integral_constant<int, 1>{});
+        float amv[TRB], bv[TRB];
+        Unroll<0, NY>::run([&](auto yc) {
+            constexpr int y = decltype(yc)::value;
+            if constexpr (y + 2 < NY) issue(std::integral_constant<int, y + 2>{});
+            const RowLd& L = rl[y];
+            const float Xe = bcast<y & 15>(xe[y >> 4]), Xl = bcast<y & 15>(xl[y >> 4]);
+            const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xe, L.Ye, kEps));
+            const float rSl = __builtin_amdgcn_rsqf(__builtin_fmaf(Xl, L.Yl, kEps));
+            const float Ae = L.ge * rSe, Al = L.gl * rSl;
+            HA[y] += Ae - Al;
+            if constexpr (y >= R && y < R + TRB) {
+                constexpr int m = y - R;
+                const float V = Ae * L.cv * rSe;
+                amv[m] = Ae * L.mp;
+                bv[m] = V * L.Ye;
+                P[1][m] = shl1_add(P[1][m], Ae * bcast<m>(mco));
+                P[2][m] = shl1_add(P[2][m], (V * af) * Xe);
+                if constexpr (m & 1)  // fold the row pair (m-1, m) of Am and B
+                    wA[m / 2] = red16(red32(amv[m - 1], bv[m - 1]), red32(amv[m], bv[m]));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        // ---- vertical box over the registers: BoxA for the 16 own rows at pixel column xb
+        float pq[TRB];
+        Unroll<0, 4>::run([&](auto mc) {
+            constexpr int m = decltype(mc)::value;
+            pq[m] = ld_bufs<float>(rPp, oPq, iso(R + m));
+        });
+        float bx = 0.f;
+#pragma unroll
+        for (int y = 0; y <= 2 * R; ++y) bx += HA[y];
+        float t1v[TRB];
+        Unroll<0, TRB>::run([&](auto mc) {
+            constexpr int m = decltype(mc)::value;
+            if constexpr (m + 4 < TRB) pq[m + 4] = ld_bufs<float>(rPp, oPq, iso(R + m + 4));
+            if constexpr (m > 0) bx = (bx + HA[m + 2 * R]) - HA[m - 1];
+            t1v[m] = (pq[m] - pb) * bx;  // p'(y0+m, xb+dl) BoxA
+            P[0][m] = shl1_add(P[0][m], bcast<m>(cxo) * bx);
+            if constexpr ((m & 3) == 3)
+                wA[8 + m / 4] = red16(red32(t1v[m - 3], t1v[m - 2]), red32(t1v[m - 1], t1v[m]));
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        const float red = reduce_tail12(wA, lane);
+        cbuf[s][qlane] = red;
+    }
+    __syncthreads();
+    flush(wfirst, nsteps);
+    __syncthreads();
+    }
+    // ---- final projector state: lane l holds column (wend - 1) + off + d0 + l
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int col = wend - 1 + (t == 0 ? -R : 0) + d0 + lane;
+        const uint32_t c4 = (col >= 0 && col < g.W) ? (uint32_t)(col * 4) : kOOB;
+        const auto rp = part_rsrc(3 + t);
+#pragma unroll
+        for (int m = 0; m < TRB; ++m)
+            st_buf(P[t][m], rp, c4 == kOOB ? kOOB : c4 + (uint32_t)(m * Wi * 4));
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(64) void k_bwd_sweep(Geo g, BwdArgs a) {
+    // Block order: tiles of kRGT consecutive row groups of one chunk, longest chunks first,
+    // dealt round-robin over the 8 XCDs (hardware block b runs on XCD b % 8): every XCD
+    // works longest-first and a tile's row groups (which re-read each other's halo rows of
+    // the gradient) share one L2.  The grid is padded to a multiple of 8 kRGT.
+    const int64_t hb = blockIdx.x, xi = hb / 8;
+    const int64_t lid = (8 * (xi / kRGT) + hb % 8) * kRGT + xi % kRGT;
+    if (lid >= (int64_t)a.nChunk * a.nsegMax * a.nRG) return;
+    const int64_t per = (int64_t)a.nsegMax * a.nRG;
+    const int j = chunk_of_rank((int)(lid / per), a.nChunk, a.jc);
+    const int sg = (int)((lid % per) / a.nRG), rg = (int)(lid % a.nRG);
+    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
+    const int64_t y0 = a.ylo + (int64_t)TRB * rg;
+    // rows y0-R .. y0+15+R all inside the volume rows: no per-row masking
+    __shared__ __attribute__((aligned(16))) float cbuf[FB][48];
+    __shared__ __attribute__((aligned(16))) float pbuf[FB][48];
+    bwd_sweep_body<K>(g, a, j, sg, rg, cbuf, pbuf);
+}
+
+// Per (range class, column): the chunks whose partials cover the column (a
+// contiguous run, since the ranges' ends are monotone in the chunk index).
+// Classes: 0 = T1c, 1 = Am/B, 2 = T1p, 3 = Ac/Bp.
+__global__ __launch_bounds__(256) void k_bwd_cover(Geo g, int64_t dlo, int nChunk, int* cover) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= g.W) return;
+    for (int cls = 0; cls < 4; ++cls) {
+        const int t = cls == 0 ? 0 : cls == 1 ? 1 : cls == 2 ? 3 : 4;
+        int first = -1, count = 0;
+        for (int j = 0; j < nChunk; ++j) {
+            int64_t lo, hi;
+            type_range(chunk_geo(g, dlo, j), g.r, t, &lo, &hi);
+            if (x >= lo && x < hi) {
+                if (first < 0) first = j;
+                ++count;
+            }
+        }
+        cover[(cls * 2) * g.W + x] = first < 0 ? 0 : first;
+        cover[(cls * 2 + 1) * g.W + x] = count;
+    }
+}
+
+// Sum the chunk partials per pixel; out (fp64, [2 sides][4][H][W]): T1, Am|Ac, B|Bp, m'*B.
+template <typename T>
+__global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* acc) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t plane = g.H * g.W;
+    if (p >= plane) return;
+    const int64_t y = p / g.W, x = p % g.W;
+    const int side = blockIdx.y;
+    double s[3] = {0.0, 0.0, 0.0};
+    if (y >= a.ylo && y < a.yhi) {
+        for (int q = 0; q < 3; ++q) {
+            const int t = 3 * side + q;
+            const int cls = 2 * side + (q == 0 ? 0 : 1);
+            const int first = a.cover[(cls * 2) * g.W + x], n = a.cover[(cls * 2 + 1) * g.W + x];
+            double v = 0.0;
+            for (int i = 0; i < n; ++i) {
+                const int j = first + i;
+                const ChunkGeo c = chunk_geo(g, a.dlo, j);
+                const int ns = chunk_nseg(c, g.r);
+                // the segment(s) of chunk j whose written range holds column x (<= 2, adjacent)
+                const int64_t rel = x - (c.wlo - g.r) - (side ? c.d0 : 0);
+                const int sa = (int)(rel >= 0 ? rel / kSeg : -((-rel + kSeg - 1) / kSeg));
+                for (int sg = sa - 1; sg <= sa + 1; ++sg) {
+                    if (sg < 0 || sg >= ns) continue;
+                    int64_t lo, hi;
+                    seg_range(c, g.r, sg, t, &lo, &hi);
+                    if (x >= lo && x < hi)
+                        v += (double)a.part[((size_t)t * a.S + 2 * (j % a.Sj) + (sg & 1)) * plane + p];
+                }
+            }
+            s[q] = v;
+        }
+    }
+    const Stats& st = side == 0 ? a.sc : a.sp;
+    const double sh = side == 0 ? (double)a.shift[0] : (double)a.shift[1];
+    const double mprime = st.box[p] / (double)(g.k * g.k) - sh;
+    double* o = acc + (size_t)side * 4 * plane;
+    o[p] = s[0];
+    o[plane + p] = s[1];
+    o[2 * plane + p] = s[2];
+    o[3 * plane + p] = s[2] * mprime;
+}
+
+// grad(y,x) = T1 - Box[A] - img'(y,x) Box[B] + Box[m' B]   (one side per blockIdx.z)
+template <typename T>
+__global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict__ cam, const T* __restrict__ proj,
+                                                      const float* __restrict__ shift, const double* __restrict__ acc,
+                                                      float* __restrict__ dcam, float* __restrict__ dproj) {
+    constexpr int TS = 16;
+    extern __shared__ __attribute__((aligned(16))) double tl[];
+    const int side = blockIdx.z;
+    float* out = side == 0 ? dcam : dproj;
+    if (!out) return;
+    const T* img = side == 0 ? cam : proj;
+    const int64_t plane = g.H * g.W;
+    const double* T1 = acc + (size_t)side * 4 * plane;
+    const double* Aa = T1 + plane;
+    const double* Bb = Aa + plane;
+    const double* MB = Bb + plane;
+    const int r = g.r, L = TS + 2 * r;
+    double* tA = tl;
+    double* tB = tA + L * L;
+    double* tM = tB + L * L;
+    const int64_t y0 = (int64_t)blockIdx.y * TS, x0 = (int64_t)blockIdx.x * TS;
+    for (int e = threadIdx.x; e < L * L; e += 256) {
+        const int64_t y = y0 + e / L - r, x = x0 + e % L - r;
+        const bool ok = y >= 0 && y < g.H && x >= 0 && x < g.W;
+        const int64_t q = y * g.W + x;
+        tA[e] = ok ? Aa[q] : 0.0;
+        tB[e] = ok ? Bb[q] : 0.0;
+        tM[e] = ok ? MB[q] : 0.0;
+    }
+    __syncthreads();
+    const int ly = threadIdx.x / TS, lx = threadIdx.x % TS;
+    const int64_t y = y0 + ly, x = x0 + lx;
+    if (y >= g.H || x >= g.W) return;
+    // separable box: rows first (k column sums per thread would re-read; k^2 adds is fine here)
+    double sa = 0, sb = 0, sm = 0;
+    for (int i = 0; i < g.k; ++i)
+        for (int jx = 0; jx < g.k; ++jx) {
+            const int e = (ly + i) * L + lx + jx;
+            sa += tA[e];
+            sb += tB[e];
+            sm += tM[e];
+        }
+    const int64_t q = y * g.W + x;
+    const double ip = (double)to_f(img[q]) - (double)shift[side];
+    out[q] = (float)(T1[q] - sa - ip * sb + sm);
+}
+
+// Image means (the global shifts cbar, pbar): per-block fp64 sums, then one block.
+template <typename T>
+__global__ __launch_bounds__(256) void k_img_blocksum(const T* __restrict__ img, int64_t n, double* bsum) {
+    __shared__ double red[256];
+    double v = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        v += (double)to_f(img[i]);
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bsum[blockIdx.x] = red[0];
+}
+__global__ __launch_bounds__(256) void k_img_shift(const double* __restrict__ bsum, int nb, int64_t n, float* shift) {
+    __shared__ double red[256];
+    for (int side = 0; side < 2; ++side) {
+        double v = 0.0;
+        for (int i = threadIdx.x; i < nb; i += 256) v += bsum[side * nb + i];
+        red[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) shift[side] = n > 0 ? (float)(red[0] / (double)n) : 0.f;
+        __syncthreads();
+    }
+}
+
+// fp32 images for the sweep (after the shifts are known): X = camera centred moment,
+// mc' = camera patch mean - cbar, c = camera; Y, mp', p likewise for the projector.  The
+// images stay unshifted so that a zero-padded (out-of-image) load minus the shift gives the
+// shifted padding value -cbar / -pbar.
+template <typename T>
+__global__ __launch_bounds__(256) void k_bwd_prep(Geo g, const T* __restrict__ cam, const T* __restrict__ proj,
+                                                  Stats sc, Stats sp, const float* __restrict__ shift, float* prep) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t plane = g.H * g.W;
+    if (p >= plane) return;
+    const double rk2 = 1.0 / (double)(g.k * g.k);
+    const float cb = shift[0], pb = shift[1];
+    prep[p] = sc.sqt[p];
+    prep[plane + p] = (float)(sc.box[p] * rk2 - (double)cb);
+    prep[2 * plane + p] = to_f(cam[p]);  // raw: the sweep subtracts cbar after a zero-padded load
+    prep[3 * plane + p] = sp.sqt[p];
+    prep[4 * plane + p] = (float)(sp.box[p] * rk2 - (double)pb);
+    prep[5 * plane + p] = to_f(proj[p]);
+}
+
+constexpr int kSumBlocks = 512;
+
+struct BwdPlan {
+    int nChunk, S, Sj, nRG, jc, nsegMax;
+    int64_t dlo, ylo, yhi;
+    size_t part_bytes, acc_bytes, cover_bytes, prep_bytes, misc_bytes;
+};
+
+BwdPlan plan_bwd(const Geo& g) {
+    BwdPlan p;
+    const int r = g.r;
+    if (g.layout == CUSTMA_LAYOUT_WINDOW) {
+        p.dlo = 0;
+        p.nChunk = (int)cdiv((int64_t)g.D + 1, NLB);
+        p.jc = 0;
+    } else {
+        p.dlo = -(g.W - 1);
+        p.nChunk = (int)cdiv(2 * g.W - 1, NLB);
+        const int64_t jc = (-32 - p.dlo) / NLB;
+        p.jc = (int)(jc < 0 ? 0 : jc >= p.nChunk ? p.nChunk - 1 : jc);
+    }
+    // slots: 2 x the max number of chunks covering one column over the four range classes
+    // (segment parity separates the overlapping projector ranges of adjacent segments)
+    p.S = 1;
+    {
+        const int64_t W = g.W;
+        int64_t* diff = (int64_t*)calloc((size_t)(W + 1), sizeof(int64_t));
+        const int ts[4] = {0, 1, 3, 4};
+        for (int c = 0; c < 4 && diff; ++c) {
+            for (int64_t x = 0; x <= W; ++x) diff[x] = 0;
+            for (int j = 0; j < p.nChunk; ++j) {
+                int64_t lo, hi;
+                type_range(chunk_geo(g, p.dlo, j), r, ts[c], &lo, &hi);
+                lo = lo < 0 ? 0 : lo;
+                hi = hi > W ? W : hi;
+                if (lo < hi) { diff[lo] += 1; diff[hi] -= 1; }
+            }
+            int64_t run = 0;
+            for (int64_t x = 0; x < W; ++x) {
+                run += diff[x];
+                if (run > p.S) p.S = (int)run;
+            }
+        }
+        free(diff);
+    }
+    p.Sj = p.S;
+    p.S = 2 * p.Sj;
+    p.nsegMax = 1;
+    for (int j = 0; j < p.nChunk; ++j) {
+        const int ns = chunk_nseg(chunk_geo(g, p.dlo, j), r);
+        if (ns > p.nsegMax) p.nsegMax = ns;
+    }
+    p.ylo = g.h_lo - r > 0 ? g.h_lo - r : 0;
+    p.yhi = g.h_hi + r < g.H ? g.h_hi + r : g.H;
+    p.nRG = (int)cdiv(p.yhi - p.ylo, TRB);
+    const size_t plane = (size_t)g.H * g.W;
+    p.part_bytes = (size_t)NTYPE * p.S * plane * sizeof(float);
+    p.acc_bytes = 8 * plane * sizeof(double);
+    p.cover_bytes = 8 * (size_t)g.W * sizeof(int);
+    p.prep_bytes = 6 * plane * sizeof(float);
+    p.misc_bytes = 2 * kSumBlocks * sizeof(double) + 256;
+    return p;
+}
+
+inline size_t a256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+template <typename T>
+hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp,
+                   float* dcam, float* dproj, void* ws, hipStream_t s) {
+    const BwdPlan p = plan_bwd(g);
+    char* w = (char*)ws;
+    float* part = (float*)w;
+    w += a256(p.part_bytes);
+    double* acc = (double*)w;
+    w += a256(p.acc_bytes);
+    int* cover = (int*)w;
+    w += a256(p.cover_bytes);
+    float* prep = (float*)w;
+    w += a256(p.prep_bytes);
+    double* bsum = (double*)w;
+    float* shift = (float*)(bsum + 2 * kSumBlocks);
+    const int64_t n = g.H * g.W;
+    hipLaunchKernelGGL(k_img_blocksum<T>, dim3(kSumBlocks), dim3(256), 0, s, cam, n, bsum);
+    hipLaunchKernelGGL(k_img_blocksum<T>, dim3(kSumBlocks), dim3(256), 0, s, proj, n, bsum + kSumBlocks);
+    hipLaunchKernelGGL(k_img_shift, dim3(1), dim3(256), 0, s, bsum, kSumBlocks, n, shift);
+    hipLaunchKernelGGL(k_bwd_cover, dim3((unsigned)cdiv(g.W, 256)), dim3(256), 0, s, g, p.dlo, p.nChunk, cover);
+    hipLaunchKernelGGL(k_bwd_prep<T>, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, g, cam, proj, sc, sp, shift, prep);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    BwdArgs a;
+    a.cam = cam; a.proj = proj; a.sc = sc; a.sp = sp;
+    a.grad = grad; a.vol = vol; a.shift = shift; a.part = part; a.cover = cover;
+    a.Xc = prep; a.mcc = prep + n; a.cc = prep + 2 * n; a.Yp = prep + 3 * n; a.mpp = prep + 4 * n; a.pp = prep + 5 * n;
+    a.S = p.S; a.Sj = p.Sj; a.nChunk = p.nChunk; a.nRG = p.nRG; a.jc = p.jc; a.nsegMax = p.nsegMax;
+    a.dlo = p.dlo; a.ylo = p.ylo; a.yhi = p.yhi;
+    const int64_t units = (int64_t)p.nChunk * p.nsegMax * p.nRG;
+    const unsigned blocks = (unsigned)(cdiv(units, 8 * kRGT) * 8 * kRGT);
+    if (units > 0) {
+        switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: hipLaunchKernelGGL((k_bwd_sweep<KK>), dim3(blocks), dim3(64), 0, s, g, a); break;
+            CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+            default: return hipErrorInvalidValue;
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc);
+    const int L = 16 + 2 * g.r;
+    hipLaunchKernelGGL(k_bwd_combine2<T>, dim3((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2), dim3(256),
+                       sizeof(double) * 3 * L * L, s, g, cam, proj, shift, acc, dcam, dproj);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t backward_workspace_bytes(const Geo& g) {
+    const BwdPlan p = plan_bwd(g);
+    return a256(p.part_bytes) + a256(p.acc_bytes) + a256(p.cover_bytes) + a256(p.prep_bytes) + a256(p.misc_bytes);
+}
+
+bool backward_supported(const Geo& g) {
+    // 32-bit buffer offsets: the volume rows one wave reads (16 + 2r + 1 row slabs) and one fp64
+    // image must stay below 2 GiB
+    const double slab = (double)g.WO * (double)g.DO * 4.0;
+    return slab * (TRB + 2 * g.r + 1) < 2147483648.0 && (double)g.H * (double)g.W * 8.0 < 2147483648.0;
+}
+
+hipError_t launch_backward(const float* grad, const float* vol, const void* cam, const void* proj, int dtype,
+                           const Geo& g, Stats sc, Stats sp, float* dcam, float* dproj, void* ws, hipStream_t s) {
+    if (dtype == CUSTMA_F16)
+        return run_bwd(grad, vol, (const __half*)cam, (const __half*)proj, g, sc, sp, dcam, dproj, ws, s);
+    return run_bwd(grad, vol, (const float*)cam, (const float*)proj, g, sc, sp, dcam, dproj, ws, s);
+}
+
+}  // namespace custma

@@ -14,7 +14,6 @@
 #include "sweep.h"
 
 namespace custma {
-size_t backward_transpose_bytes(const Geo& g);
 
 namespace {
 thread_local char g_err[512] = "";
@@ -63,6 +62,8 @@ int set_band(Geo* g, int64_t row_begin, int64_t row_end) {
 
 size_t stats_bytes(const Geo& g) { return 2 * align256((size_t)g.H * g.W * 20); }
 
+size_t volume_bytes(const Geo& g) { return (size_t)g.HV() * g.WO * g.DO * sizeof(float); }
+
 void carve_stats(const Geo& g, void* ws, Stats* sc, Stats* sp) {
     const size_t n = (size_t)g.H * g.W;
     char* p = (char*)ws;
@@ -107,7 +108,7 @@ using namespace custma;
 
 extern "C" {
 
-int custma_abi_version(void) { return 1; }
+int custma_abi_version(void) { return 2; }
 
 const char* custma_last_error(void) { return g_err; }
 
@@ -125,7 +126,8 @@ size_t custma_workspace_bytes(int64_t H, int64_t W, int32_t kernel_size, int32_t
     if (make_geo(H, W, kernel_size, layout, D, &g)) return 0;
     size_t n = stats_bytes(g);
     if (op == CUSTMA_OP_DISPARITY) n += align256(disparity_partial_bytes(g));
-    if (op == CUSTMA_OP_BACKWARD) n += align256(backward_partial_bytes(g)) + align256(backward_transpose_bytes(g));
+    if (op == CUSTMA_OP_BACKWARD || op == CUSTMA_OP_BACKWARD_RECOMPUTE) n += align256(backward_workspace_bytes(g));
+    if (op == CUSTMA_OP_BACKWARD_RECOMPUTE) n += align256(volume_bytes(g));
     return n;
 }
 
@@ -156,39 +158,47 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     return check_hip(launch_fwd_exact(camera, projector, dtype, g, sc, sp, cost_volume, s), "forward(exact)");
 }
 
-int custma_backward(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
-                    int64_t W, int32_t kernel_size, int32_t layout, int32_t D, float* camera_grad,
-                    float* projector_grad, void* workspace, size_t workspace_bytes, void* stream) {
-    return custma_backward_band(grad, camera, projector, dtype, H, W, kernel_size, layout, D, 0, H, camera_grad,
-                                projector_grad, workspace, workspace_bytes, stream);
+int custma_backward(const float* grad, const float* cost_volume, const void* camera, const void* projector,
+                    int32_t dtype, int64_t H, int64_t W, int32_t kernel_size, int32_t layout, int32_t D,
+                    float* camera_grad, float* projector_grad, void* workspace, size_t workspace_bytes, void* stream) {
+    return custma_backward_band(grad, cost_volume, camera, projector, dtype, H, W, kernel_size, layout, D, 0, H,
+                                camera_grad, projector_grad, workspace, workspace_bytes, stream);
 }
 
-int custma_backward_band(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
-                         int64_t W, int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin,
-                         int64_t row_end, float* camera_grad, float* projector_grad, void* workspace,
-                         size_t workspace_bytes, void* stream) {
+int custma_backward_band(const float* grad, const float* cost_volume, const void* camera, const void* projector,
+                         int32_t dtype, int64_t H, int64_t W, int32_t kernel_size, int32_t layout, int32_t D,
+                         int64_t row_begin, int64_t row_end, float* camera_grad, float* projector_grad,
+                         void* workspace, size_t workspace_bytes, void* stream) {
     Geo g;
     int rc = make_geo(H, W, kernel_size, layout, D, &g);
     if (rc || (rc = check_dtype(dtype)) || (rc = set_band(&g, row_begin, row_end))) return rc;
     if (!fast_supported(g.k))
         return fail(CUSTMA_E_UNSUPPORTED, "backward supports odd kernel_size <= 15, got %d", g.k);
+    if (!backward_supported(g))
+        return fail(CUSTMA_E_UNSUPPORTED, "backward: a volume row (W_out x D_out floats) must stay below 2 GiB");
     if (g.H == 0 || g.W == 0 || (!camera_grad && !projector_grad)) return CUSTMA_OK;
+    hipStream_t s = (hipStream_t)stream;
     if (g.HV() == 0) {  // no volume rows: gradients are zero
-        hipStream_t s0 = (hipStream_t)stream;
-        if (camera_grad) rc = check_hip(hipMemsetAsync(camera_grad, 0, sizeof(float) * g.H * g.W, s0), "memset");
+        if (camera_grad) rc = check_hip(hipMemsetAsync(camera_grad, 0, sizeof(float) * g.H * g.W, s), "memset");
         if (!rc && projector_grad)
-            rc = check_hip(hipMemsetAsync(projector_grad, 0, sizeof(float) * g.H * g.W, s0), "memset");
+            rc = check_hip(hipMemsetAsync(projector_grad, 0, sizeof(float) * g.H * g.W, s), "memset");
         return rc;
     }
     if (!grad || !camera || !projector || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
-    const size_t need = stats_bytes(g) + align256(backward_partial_bytes(g)) +
-                        (projector_grad ? align256(backward_transpose_bytes(g)) : 0);
+    const size_t need = stats_bytes(g) + align256(backward_workspace_bytes(g)) +
+                        (cost_volume ? 0 : align256(volume_bytes(g)));
     if (workspace_bytes < need) return fail(CUSTMA_E_WORKSPACE, "workspace too small (%zu < %zu)", workspace_bytes, need);
-    hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
     if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
-    void* ws2 = (char*)workspace + stats_bytes(g);
-    return check_hip(launch_backward(grad, camera, projector, dtype, g, sc, sp, camera_grad, projector_grad, ws2, s),
+    char* ws2 = (char*)workspace + stats_bytes(g);
+    if (!cost_volume) {  // recompute the forward (fast path) into the workspace
+        float* vol = (float*)(ws2 + align256(backward_workspace_bytes(g)));
+        if ((rc = check_hip(launch_fwd_fast(camera, projector, dtype, g, sc, sp, vol, s), "backward(recompute)")))
+            return rc;
+        cost_volume = vol;
+    }
+    return check_hip(launch_backward(grad, cost_volume, camera, projector, dtype, g, sc, sp, camera_grad,
+                                     projector_grad, ws2, s),
                      "backward");
 }
 

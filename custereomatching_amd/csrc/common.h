@@ -94,6 +94,23 @@ __device__ __forceinline__ float ld_buf<__half>(__amdgpu_buffer_rsrc_t r, uint32
 __device__ __forceinline__ double ld_buf_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
+// Same with a wave-uniform byte offset `so` (SGPR soffset) added to the address.  Callers keep
+// so + (any in-range voffset) below the descriptor's num_records, so an out-of-range voffset
+// (0x80000000) reads 0 whether or not the hardware range check includes soffset.
+template <typename T>
+__device__ __forceinline__ float ld_bufs(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t so);
+template <>
+__device__ __forceinline__ float ld_bufs<float>(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, so, 0));
+}
+template <>
+__device__ __forceinline__ float ld_bufs<__half>(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t so) {
+    const unsigned short b = __builtin_amdgcn_raw_buffer_load_b16(r, off, so, 0);
+    return __half2float(__ushort_as_half(b));
+}
+__device__ __forceinline__ double ld_bufs_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t so) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, so, 0));
+}
 #ifndef CUSTMA_STORE_AUX
 #define CUSTMA_STORE_AUX 0  // cache-policy bits of the volume stores (gfx950: 1 sc0, 2 nt, 16 sc1)
 #endif
@@ -114,8 +131,9 @@ hipError_t launch_argmax(const float* vol, int64_t rows, int64_t n, int64_t* idx
 size_t disparity_partial_bytes(const Geo& g);
 hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             int64_t* idx, float* best, int32_t* n_rechecked, void* ws, hipStream_t s);
-size_t backward_partial_bytes(const Geo& g);
-hipError_t launch_backward(const float* grad, const void* cam, const void* proj, int dtype, const Geo& g,
-                           Stats sc, Stats sp, float* dcam, float* dproj, void* ws, hipStream_t s);
+size_t backward_workspace_bytes(const Geo& g);
+bool backward_supported(const Geo& g);
+hipError_t launch_backward(const float* grad, const float* vol, const void* cam, const void* proj, int dtype,
+                           const Geo& g, Stats sc, Stats sp, float* dcam, float* dproj, void* ws, hipStream_t s);
 bool fast_supported(int k);
 }  // namespace custma

@@ -2,9 +2,26 @@
 #pragma once
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace custma {
+
+// Compile-time loop: f(std::integral_constant<int, X>) for X in [X0, NX).
+template <int X, int NX>
+struct Unroll {
+    template <typename F>
+    __device__ __forceinline__ static void run(F&& f) {
+        f(std::integral_constant<int, X>{});
+        Unroll<X + 1, NX>::run(f);
+    }
+};
+template <int NX>
+struct Unroll<NX, NX> {
+    template <typename F>
+    __device__ __forceinline__ static void run(F&&) {}
+};
 
 constexpr int TW = 16;  // camera (own-image) columns per workgroup
 

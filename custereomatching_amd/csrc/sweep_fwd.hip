@@ -55,19 +55,6 @@ __device__ __forceinline__ void fmac_bc32(float& acc, float a, float b) {
 }
 typedef __attribute__((address_space(3))) volatile double lds_vd;
 
-template <int X, int NX>
-struct Unroll {
-    template <typename F>
-    __device__ __forceinline__ static void run(F&& f) {
-        f(std::integral_constant<int, X>{});
-        Unroll<X + 1, NX>::run(f);
-    }
-};
-template <int NX>
-struct Unroll<NX, NX> {
-    template <typename F>
-    __device__ __forceinline__ static void run(F&&) {}
-};
 
 template <int K, int TWT, typename T, bool ARGMAX>
 __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,

@@ -44,11 +44,11 @@ class HipBackend:
 
         return cost_volume_forward(cam, proj, D, k, layout, precision, rows=rows)
 
-    def backward(self, grad, cam, proj, D, k, layout, rows, want_cam, want_proj):
+    def backward(self, grad, cam, proj, D, k, layout, rows, want_cam, want_proj, vol=None):
         from .stereo_matching_wrapper import cost_volume_backward
 
         return cost_volume_backward(grad, cam, proj, k, layout, D, camera_grad=want_cam,
-                                    projector_grad=want_proj, rows=rows)
+                                    projector_grad=want_proj, rows=rows, cost_volume=vol)
 
     def disparity(self, cam, proj, D, k, layout, rows):
         from .disparity import stereo_disparity
@@ -131,16 +131,16 @@ class _RowBandStereoMatching(torch.autograd.Function):
         top, _ = rbg.halo_sizes()
         n = cam_band.shape[0]
         vol = backend.forward(ch, ph, D, kernel_size, layout, precision, (top, top + n))
-        ctx.save_for_backward(ch, ph)
+        ctx.save_for_backward(ch, ph, vol)
         ctx.meta = (D, kernel_size, layout, rbg, backend, top, n)
         return vol
 
     @staticmethod
     def backward(ctx, grad):
-        ch, ph = ctx.saved_tensors
+        ch, ph, vol = ctx.saved_tensors
         D, k, layout, rbg, backend, top, n = ctx.meta
         want_c, want_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        gc, gp = backend.backward(grad.contiguous(), ch, ph, D, k, layout, (top, top + n), want_c, want_p)
+        gc, gp = backend.backward(grad.contiguous(), ch, ph, D, k, layout, (top, top + n), want_c, want_p, vol)
         gc = rbg.reduce_halo(gc, n) if gc is not None else None
         gp = rbg.reduce_halo(gp, n) if gp is not None else None
         return gc, gp, None, None, None, None, None, None

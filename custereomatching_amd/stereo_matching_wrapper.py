@@ -135,12 +135,15 @@ def cost_volume_forward(camera: torch.Tensor, projector: torch.Tensor, D: int, k
 
 def cost_volume_backward(cost_volume_grad: torch.Tensor, camera: torch.Tensor, projector: torch.Tensor,
                          kernel_size: int, layout: str = "full", D: int = 0, camera_grad: bool = True,
-                         projector_grad: bool = False, rows: Optional[Tuple[int, int]] = None
+                         projector_grad: bool = False, rows: Optional[Tuple[int, int]] = None,
+                         cost_volume: Optional[torch.Tensor] = None
                          ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
     """Gradients of sum(grad * volume) (reference: stereo::stereo_matching_backward,
-    custma/src/stereo_matching.cpp:45-73; camera only there).  With ``rows=(b, e)``
-    the grad covers volume rows [b, e) of a haloed band and the returned image
-    gradients cover every buffer row (halo rows hold partial sums)."""
+    custma/src/stereo_matching.cpp:45-73; camera only there).  ``cost_volume`` is the
+    forward's output for these images (the autograd op passes the one it returned);
+    without it the library recomputes it in its workspace.  With ``rows=(b, e)`` the
+    grad covers volume rows [b, e) of a haloed band and the returned image gradients
+    cover every buffer row (halo rows hold partial sums)."""
     _check_input(cost_volume_grad, "cost_volume_grad")
     code = _check_pair(camera, projector, kernel_size)
     lay = _LAYOUTS[layout]
@@ -148,24 +151,31 @@ def cost_volume_backward(cost_volume_grad: torch.Tensor, camera: torch.Tensor, p
     r0, r1 = _rows(H, rows)
     Dl = int(D) if lay == _lib.LAYOUT_WINDOW else 0
     WO, DO = _lib.volume_dims(H, W, lay, Dl)
-    if tuple(cost_volume_grad.shape) != (r1 - r0, WO, DO):
-        raise RuntimeError(f"cost_volume_grad shape {tuple(cost_volume_grad.shape)} != volume shape "
-                           f"{(r1 - r0, WO, DO)}")
+    vshape = (r1 - r0, WO, DO)
+    if tuple(cost_volume_grad.shape) != vshape:
+        raise RuntimeError(f"cost_volume_grad shape {tuple(cost_volume_grad.shape)} != volume shape {vshape}")
     if cost_volume_grad.dtype != torch.float32:
         raise RuntimeError(f"expected scalar type Float but found {cost_volume_grad.dtype}")
+    if cost_volume is not None:
+        _check_input(cost_volume, "cost_volume")
+        if tuple(cost_volume.shape) != vshape or cost_volume.dtype != torch.float32:
+            raise RuntimeError(f"cost_volume must be a float32 tensor of shape {vshape}")
     dev = camera.device
     gc = torch.empty((H, W), dtype=torch.float32, device=dev) if camera_grad else None
     gp = torch.empty((H, W), dtype=torch.float32, device=dev) if projector_grad else None
     if H * W == 0 or (gc is None and gp is None):
         return (gc.zero_() if gc is not None else None), (gp.zero_() if gp is not None else None)
     with torch.cuda.device(dev):
-        nb = _lib.workspace_bytes(H, W, kernel_size, lay, Dl, _lib.OP_BACKWARD)
+        op = _lib.OP_BACKWARD if cost_volume is not None else _lib.OP_BACKWARD_RECOMPUTE
+        nb = _lib.workspace_bytes(H, W, kernel_size, lay, Dl, op)
         ws = _workspace(nb, dev)
-        _lib.check(_lib.lib.custma_backward_band(cost_volume_grad.data_ptr(), camera.data_ptr(),
-                                                 projector.data_ptr(), code, H, W, kernel_size, lay, Dl, r0, r1,
-                                            gc.data_ptr() if gc is not None else None,
-                                            gp.data_ptr() if gp is not None else None,
-                                            ws.data_ptr(), ws.numel(), _stream_ptr(dev)),
+        _lib.check(_lib.lib.custma_backward_band(cost_volume_grad.data_ptr(),
+                                                 cost_volume.data_ptr() if cost_volume is not None else None,
+                                                 camera.data_ptr(), projector.data_ptr(), code, H, W, kernel_size,
+                                                 lay, Dl, r0, r1,
+                                                 gc.data_ptr() if gc is not None else None,
+                                                 gp.data_ptr() if gp is not None else None,
+                                                 ws.data_ptr(), ws.numel(), _stream_ptr(dev)),
                    "stereo_matching_backward")
     return gc, gp
 
@@ -175,19 +185,21 @@ class _StereoMatching(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, camera_image, projector_image, D, kernel_size, layout="full", precision=None):
-        ctx.save_for_backward(camera_image, projector_image)
+        vol = cost_volume_forward(camera_image, projector_image, D, kernel_size, layout, precision)
+        # the backward reads the returned volume (V = g * cost / S); saved like any output
+        ctx.save_for_backward(camera_image, projector_image, vol)
         ctx.D = D
         ctx.kernel_size = kernel_size
         ctx.layout = layout
-        return cost_volume_forward(camera_image, projector_image, D, kernel_size, layout, precision)
+        return vol
 
     @staticmethod
     def backward(ctx, cost_volume_grad):
-        camera_image, projector_image = ctx.saved_tensors
+        camera_image, projector_image, vol = ctx.saved_tensors
         want_c, want_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         gc, gp = cost_volume_backward(cost_volume_grad.contiguous(), camera_image, projector_image,
                                       ctx.kernel_size, ctx.layout, ctx.D, camera_grad=want_c,
-                                      projector_grad=want_p)
+                                      projector_grad=want_p, cost_volume=vol)
         if gc is not None and camera_image.dtype != torch.float32:
             gc = gc.to(camera_image.dtype)
         if gp is not None and projector_image.dtype != torch.float32:

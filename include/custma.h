@@ -43,6 +43,7 @@ extern "C" {
 #define CUSTMA_OP_FORWARD 0
 #define CUSTMA_OP_BACKWARD 1
 #define CUSTMA_OP_DISPARITY 2
+#define CUSTMA_OP_BACKWARD_RECOMPUTE 3 /* custma_backward with cost_volume == NULL */
 
 /* error codes */
 #define CUSTMA_OK 0
@@ -54,7 +55,7 @@ extern "C" {
 
 #define CUSTMA_MAX_KERNEL 31
 
-int custma_abi_version(void);
+int custma_abi_version(void); /* 2 */
 const char* custma_last_error(void);
 
 /* Volume dims for a layout: *wo = W (full) or W-D (window); *dout = W or D+1. */
@@ -76,11 +77,13 @@ int custma_forward(const void* camera, const void* projector, int32_t dtype, int
  * Replaces stereo::stereo_matching_backward (custma/src/stereo_matching.cpp:45-73) and
  * stereo_matching_backward_wrapper + get_patches_grad_kernel + patches_grad_to_image_kernel
  * (custma/src/stereo_matching_kernel.cu:75-179, :218-261).  Deterministic (no atomics).
+ * `cost_volume` is the forward's output for the same images (the autograd op keeps it); NULL makes
+ * the call recompute it into the workspace (size the workspace with CUSTMA_OP_BACKWARD_RECOMPUTE).
  * camera_grad / projector_grad may each be NULL (not computed); the reference computes the
  * camera gradient only (custma/stereo_matching_wrapper.py:33). */
-int custma_backward(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
-                    int64_t W, int32_t kernel_size, int32_t layout, int32_t D, float* camera_grad,
-                    float* projector_grad, void* workspace, size_t workspace_bytes, void* stream);
+int custma_backward(const float* grad, const float* cost_volume, const void* camera, const void* projector,
+                    int32_t dtype, int64_t H, int64_t W, int32_t kernel_size, int32_t layout, int32_t D,
+                    float* camera_grad, float* projector_grad, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Row-band variants (multi-GPU row sharding): the image buffers hold H rows -- a band plus
  * its halo -- and only volume rows [row_begin, row_end) are produced / consumed.  The volume (and grad)
@@ -91,10 +94,10 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
                         int32_t kernel_size, int32_t layout, int32_t D, int32_t precision, int64_t row_begin,
                         int64_t row_end, float* cost_volume, void* workspace, size_t workspace_bytes,
                         void* stream);
-int custma_backward_band(const float* grad, const void* camera, const void* projector, int32_t dtype, int64_t H,
-                         int64_t W, int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin,
-                         int64_t row_end, float* camera_grad, float* projector_grad, void* workspace,
-                         size_t workspace_bytes, void* stream);
+int custma_backward_band(const float* grad, const float* cost_volume, const void* camera, const void* projector,
+                         int32_t dtype, int64_t H, int64_t W, int32_t kernel_size, int32_t layout, int32_t D,
+                         int64_t row_begin, int64_t row_end, float* camera_grad, float* projector_grad,
+                         void* workspace, size_t workspace_bytes, void* stream);
 int custma_disparity_band(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
                           int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin, int64_t row_end,
                           int64_t* index, float* best, int32_t* n_rechecked, void* workspace,

@@ -29,17 +29,17 @@ def run(name, ops, reps):
             res[f"fwd_{prec}_GBps"] = round(nb / ms / 1e6, 1)
             del out
     if "bwd" in ops:
-        WO = W if lay == "full" else W - D
-        DO = W if lay == "full" else D + 1
-        g = torch.rand(H, WO, DO, device="cuda") - 0.5
-        cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True)
+        vol = cm.cost_volume_forward(cam, proj, D, k, lay, "fast")
+        g = torch.rand_like(vol) - 0.5
+        cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True, cost_volume=vol)
         et = EventTimer()
         for _ in range(reps):
-            et.record(lambda: cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True))
+            et.record(lambda: cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True,
+                                                      cost_volume=vol))
         ms = et.mean_ms()
         res["bwd_ms"] = round(ms, 4)
-        res["bwd_GBps_g"] = round(g.numel() * 4 / ms / 1e6, 1)
-        del g
+        res["bwd_GBps_g_vol"] = round(2 * g.numel() * 4 / ms / 1e6, 1)
+        del g, vol
     if "disp" in ops:
         cm.stereo_disparity(cam, proj, D, k, lay)
         et = EventTimer()

@@ -43,7 +43,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_and_dims():
     from custereomatching_amd import _lib
 
-    assert _lib.lib.custma_abi_version() == 1
+    assert _lib.lib.custma_abi_version() == 2
     assert _lib.volume_dims(128, 256, _lib.LAYOUT_FULL, 0) == (256, 256)
     assert _lib.volume_dims(128, 256, _lib.LAYOUT_WINDOW, 32) == (224, 33)
     with pytest.raises(ValueError):
@@ -70,7 +70,7 @@ def test_entry_points_validate_before_launch():
     assert L.custma_forward(None, None, 0, 8, 8, 5, 1, 8, 1, None, None, 0, None) == _lib.E_ARG  # D >= W
     assert L.custma_forward(None, None, 0, 8, 8, 5, 0, 0, 1, None, None, 0, None) == _lib.E_NULL
     assert L.custma_forward(None, None, 0, 0, 8, 5, 0, 0, 1, None, None, 0, None) == 0  # empty image: no-op
-    assert L.custma_backward(None, None, None, 0, 8, 8, 17, 0, 0, None, None, None, 0, None) == _lib.E_UNSUPPORTED
+    assert L.custma_backward(None, None, None, None, 0, 8, 8, 17, 0, 0, None, None, None, 0, None) == _lib.E_UNSUPPORTED
     assert L.custma_argmax(None, 4, 0, None, None, None) == _lib.E_ARG
     assert L.custma_disparity(None, None, 0, 8, 8, 5, 0, 0, None, None, None, None, 0, None) == _lib.E_NULL
 

@@ -312,3 +312,34 @@ def test_band_api_matches_whole_image(gpu, layout, D):
         assert torch.equal(ib, vi) and torch.equal(bb, vb2)
     assert float((acc_c - rc).abs().max()) <= 1e-5 * max(1.0, float(rc.abs().max()))
     assert float((acc_p - rp).abs().max()) <= 1e-5 * max(1.0, float(rp.abs().max()))
+
+
+@pytest.mark.parametrize("layout,D", [(FULL, 0), (WIN, 20)])
+def test_backward_given_volume_matches_recompute(gpu, layout, D):
+    """The autograd op hands the forward's volume to the backward (V = g * cost / S); the
+    recompute path (no volume, the reference's backward signature) must agree with it."""
+    H, W, k = 37, 90, 11
+    cam, proj = make_pair(H, W, max(D, 1), seed=61, kind="smooth")
+    c, p = _dev(cam, gpu), _dev(proj, gpu)
+    vol = cm.cost_volume_forward(c, p, D, k, layout, "fast")
+    g = _dev(_rand_grad(tuple(vol.shape), 62), gpu)
+    a = cm.cost_volume_backward(g, c, p, k, layout, D, projector_grad=True, cost_volume=vol)
+    b = cm.cost_volume_backward(g, c, p, k, layout, D, projector_grad=True)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    lay, Dl = _layout_args(layout, D)
+    rc, rp = O.backward_f64(g.cpu().numpy(), cam, proj, k, layout=lay, D=Dl)
+    assert np.abs(a[0].cpu().numpy() - rc).max() <= 1e-5 * max(1, np.abs(rc).max())
+    assert np.abs(a[1].cpu().numpy() - rp).max() <= 1e-5 * max(1, np.abs(rp).max())
+
+
+def test_backward_wide_full_layout_many_chunks(gpu):
+    """Full layout with W = 300: 10 diagonal chunks of 64, several partial slots per column,
+    and row groups that straddle the volume edge."""
+    H, W, k = 45, 300, 9
+    cam, proj = make_pair(H, W, 40, seed=71)
+    g = _rand_grad((H, W, W), 72)
+    rc, rp = O.backward_f64(g, cam, proj, k)
+    gc, gp = cm.cost_volume_backward(_dev(g, gpu), _dev(cam, gpu), _dev(proj, gpu), k, projector_grad=True)
+    assert np.abs(gc.cpu().numpy() - rc).max() <= 1e-5 * max(1, np.abs(rc).max())
+    assert np.abs(gp.cpu().numpy() - rp).max() <= 1e-5 * max(1, np.abs(rp).max())

@@ -34,7 +34,7 @@ class OracleBackend:
         v = O.forward(cam.numpy(), proj.numpy(), k, layout=lay, D=Dl)
         return torch.from_numpy(v[rows[0]:rows[1]].copy())
 
-    def backward(self, grad, cam, proj, D, k, layout, rows, want_cam, want_proj):
+    def backward(self, grad, cam, proj, D, k, layout, rows, want_cam, want_proj, vol=None):
         lay, Dl = self._lay(layout, D)
         H, W = cam.shape
         g = np.zeros(O.volume_shape(H, W, lay, Dl), np.float32)
