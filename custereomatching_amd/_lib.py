@@ -22,7 +22,7 @@ E_ARG, E_NULL, E_WORKSPACE, E_LAUNCH, E_UNSUPPORTED = -1, -2, -3, -4, -5
 
 EXPORTS = ("custma_abi_version", "custma_last_error", "custma_volume_dims", "custma_workspace_bytes",
            "custma_forward", "custma_backward", "custma_argmax", "custma_disparity", "custma_forward_band",
-           "custma_backward_band", "custma_disparity_band")
+           "custma_backward_band", "custma_disparity_band", "custma_profile_enable", "custma_profile_mean_ms")
 
 
 class CustmaError(RuntimeError):
@@ -33,7 +33,7 @@ def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"custereomatching_amd: HIP library not found at {LIB_PATH}; build it with "
-            "`python -m custereomatching_amd.build` (hipcc, gfx950). There is no CPU fallback.")
+            "`python custereomatching_amd/build.py` (hipcc, gfx950). There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH)
     vp, i64, i32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_size_t
     i64p = ctypes.POINTER(ctypes.c_int64)
@@ -51,7 +51,9 @@ def _load():
                                          vp]
     lib.custma_disparity_band.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, vp, vp, vp, vp, sz,
                                           vp]
-    for name in ("custma_forward", "custma_backward", "custma_argmax", "custma_disparity",
+    lib.custma_profile_enable.argtypes = [i32]
+    lib.custma_profile_mean_ms.argtypes = [i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int32)]
+    for name in ("custma_profile_enable", "custma_profile_mean_ms", "custma_forward", "custma_backward", "custma_argmax", "custma_disparity",
                  "custma_volume_dims", "custma_forward_band", "custma_backward_band", "custma_disparity_band"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
@@ -77,3 +79,18 @@ def volume_dims(H: int, W: int, layout: int, D: int):
 
 def workspace_bytes(H, W, k, layout, D, op) -> int:
     return int(lib.custma_workspace_bytes(H, W, k, layout, D, op))
+
+
+PROF_FWD, PROF_BWD = 0, 1
+
+
+def profile_enable(on: bool) -> None:
+    """HIP-event timing of the main kernel of each op (bench only; see include/custma.h)."""
+    check(lib.custma_profile_enable(1 if on else 0), "profile_enable")
+
+
+def profile_mean_ms(which: int):
+    """(mean kernel ms, launches) since profile_enable(True); clears the collection."""
+    ms, n = ctypes.c_float(), ctypes.c_int32()
+    check(lib.custma_profile_mean_ms(which, ctypes.byref(ms), ctypes.byref(n)), "profile_mean_ms")
+    return float(ms.value), int(n.value)

@@ -1,5 +1,5 @@
 """Build libcustma_hip.so for gfx950 with hipcc (in-tree, so it travels with
-the repo snapshot to the GPU box).  Usage: python -m custereomatching_amd.build
+the repo snapshot to the GPU box).  Usage: python custereomatching_amd/build.py [--force]
 
 Each .hip translation unit is compiled separately (parallel) and linked
 into one shared library exporting the C ABI of include/custma.h.

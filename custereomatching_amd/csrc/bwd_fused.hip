@@ -51,9 +51,18 @@ constexpr int TRB = 16;   // own rows per wave
 constexpr int NLB = 64;   // diagonals per wave
 constexpr int FB = 16;    // steps per flush
 constexpr int NTYPE = 6;  // partial types: T1c, Am, B (camera) | T1p, Ac, Bp (projector)
-constexpr int kRGT = 4;   // row groups per XCD tile
 constexpr int kSeg = 128; // pixel columns per wave (>= 64 + 2 r: segments s and s+2 never overlap)
 constexpr uint32_t kOOB = 0x80000000u;
+#ifndef CUSTMA_BWD_PF
+#define CUSTMA_BWD_PF 2
+#endif
+constexpr int kPF = CUSTMA_BWD_PF;  // rows of loads in flight ahead of the row being computed
+#ifndef CUSTMA_BWD_VAUX
+#define CUSTMA_BWD_VAUX 0  // cache-policy bits of the gradient / volume loads (gfx950: 1 sc0, 2 nt, 16 sc1)
+#endif
+__device__ __forceinline__ float ld_vol(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, so, CUSTMA_BWD_VAUX));
+}
 
 // Chunk geometry (host and device): diagonals [d0, d0+64); camera columns that carry
 // a valid voxel for some lane: [wlo, whi); pixel columns whose box touches one:
@@ -117,7 +126,7 @@ struct BwdArgs {
     const float* vol;
     const float* shift;  // [2]: cbar, pbar
     float* part;         // [NTYPE][S][H][W]
-    const int* cover;    // [4][2][W]: first chunk, count per (range class, column)
+    const int* cover;    // k_bwd_cover: slot counts and lists per (range class, column)
     int S, Sj, nChunk, nRG, jc, nsegMax;
     int64_t dlo, ylo, yhi;
 };
@@ -304,7 +313,7 @@ __device__ __forceinline__ void bwd_sweep_body(const Geo& g, const BwdArgs& a, i
         };
 
         // ---- A entering (column w) and leaving (column w - k) on the NY rows; the loads of
-        // row y + 2 are issued before row y is computed (sched barriers keep that order and
+        // row y + kPF are issued before row y is computed (sched barriers keep that order and
         // stop the scheduler from hoisting all rows' loads, which would pin ~150 VGPRs)
         struct RowLd {
             float ge, gl, Ye, Yl, cv, mp;
@@ -313,21 +322,33 @@ __device__ __forceinline__ void bwd_sweep_body(const Geo& g, const BwdArgs& a, i
         auto issue = [&](auto yc) {
             constexpr int y = decltype(yc)::value;
             const uint32_t so = vso(y), sy = iso(y);
-            rl[y].ge = ld_bufs<float>(rG, oGe, so);
-            rl[y].gl = ld_bufs<float>(rG, oGl, so);
+            rl[y].ge = ld_vol(rG, oGe, so);
+#ifndef CUSTMA_ABL_NOLEAVE  // ablation builds only (scripts/build_ablations.py)
+            rl[y].gl = ld_vol(rG, oGl, so);
+#else
+            rl[y].gl = 0.f;
+#endif
+#ifndef CUSTMA_ABL_NOIMG
             rl[y].Ye = ld_bufs<float>(rYp, oYe, sy);
             rl[y].Yl = ld_bufs<float>(rYp, oYl, sy);
+#else
+            rl[y].Ye = 1.f + (float)y;
+            rl[y].Yl = 1.f;
+#endif
             if constexpr (y >= R && y < R + TRB) {
-                rl[y].cv = ld_bufs<float>(rV, oGe, so);
+                rl[y].cv = ld_vol(rV, oGe, so);
+#ifndef CUSTMA_ABL_NOIMG
                 rl[y].mp = ld_bufs<float>(rMp, oYe, sy);
+#else
+                rl[y].mp = 0.5f;
+#endif
             }
         };
-        issue(std::integral_constant<int, 0>{});
-        if constexpr (NY > 1) issue(std::integral_constant<int, 1>{});
+        Unroll<0, (kPF < NY ? kPF : NY)>::run([&](auto yc) { issue(yc); });
         float amv[TRB], bv[TRB];
         Unroll<0, NY>::run([&](auto yc) {
             constexpr int y = decltype(yc)::value;
-            if constexpr (y + 2 < NY) issue(std::integral_constant<int, y + 2>{});
+            if constexpr (y + kPF < NY) issue(std::integral_constant<int, y + kPF>{});
             const RowLd& L = rl[y];
             const float Xe = bcast<y & 15>(xe[y >> 4]), Xl = bcast<y & 15>(xl[y >> 4]);
             const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xe, L.Ye, kEps));
@@ -366,7 +387,13 @@ __device__ __forceinline__ void bwd_sweep_body(const Geo& g, const BwdArgs& a, i
                 wA[8 + m / 4] = red16(red32(t1v[m - 3], t1v[m - 2]), red32(t1v[m - 1], t1v[m]));
             __builtin_amdgcn_sched_barrier(0);
         });
+#ifndef CUSTMA_ABL_NORED
         const float red = reduce_tail12(wA, lane);
+#else
+        float red = 0.f;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) red += wA[i];
+#endif
         cbuf[s][qlane] = red;
     }
     __syncthreads();
@@ -387,47 +414,53 @@ __device__ __forceinline__ void bwd_sweep_body(const Geo& g, const BwdArgs& a, i
 
 template <int K>
 __global__ __launch_bounds__(64) void k_bwd_sweep(Geo g, BwdArgs a) {
-    // Block order: tiles of kRGT consecutive row groups of one chunk, longest chunks first,
-    // dealt round-robin over the 8 XCDs (hardware block b runs on XCD b % 8): every XCD
-    // works longest-first and a tile's row groups (which re-read each other's halo rows of
-    // the gradient) share one L2.  The grid is padded to a multiple of 8 kRGT.
-    const int64_t hb = blockIdx.x, xi = hb / 8;
-    const int64_t lid = (8 * (xi / kRGT) + hb % 8) * kRGT + xi % kRGT;
-    if (lid >= (int64_t)a.nChunk * a.nsegMax * a.nRG) return;
-    const int64_t per = (int64_t)a.nsegMax * a.nRG;
-    const int j = chunk_of_rank((int)(lid / per), a.nChunk, a.jc);
-    const int sg = (int)((lid % per) / a.nRG), rg = (int)(lid % a.nRG);
+    // Block order: XCD x (hardware block b runs on XCD b % 8) owns the row groups
+    // [x nRGx, (x+1) nRGx) and runs every (chunk, segment) unit on them, longest chunks
+    // first; so an XCD's L2 holds only its rows of the images, and the halo rows a
+    // wave re-reads from its neighbour row groups' gradient are read on the same XCD.
+    const int64_t hb = blockIdx.x, xi = hb / 8, x = hb % 8;
+    const int nRGx = (a.nRG + 7) / 8;
+    const int64_t unit = xi / nRGx;
+    const int rg = (int)(x * nRGx + xi % nRGx);
+    if (rg >= a.nRG || unit >= (int64_t)a.nChunk * a.nsegMax) return;
+    const int j = chunk_of_rank((int)(unit / a.nsegMax), a.nChunk, a.jc);
+    const int sg = (int)(unit % a.nsegMax);
     if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
-    const int64_t y0 = a.ylo + (int64_t)TRB * rg;
-    // rows y0-R .. y0+15+R all inside the volume rows: no per-row masking
     __shared__ __attribute__((aligned(16))) float cbuf[FB][48];
     __shared__ __attribute__((aligned(16))) float pbuf[FB][48];
     bwd_sweep_body<K>(g, a, j, sg, rg, cbuf, pbuf);
 }
 
-// Per (range class, column): the chunks whose partials cover the column (a
-// contiguous run, since the ranges' ends are monotone in the chunk index).
-// Classes: 0 = T1c, 1 = Am/B, 2 = T1p, 3 = Ac/Bp.
-__global__ __launch_bounds__(256) void k_bwd_cover(Geo g, int64_t dlo, int nChunk, int* cover) {
+// Per (range class, column): the partial slots that hold the column (class 0 = camera
+// T1c / Am / B, which share one range; 1 = projector T1p; 2 = projector Ac / Bp).
+// cover layout: [3][W] counts, then [3][W][S] slot indices (uint16).
+__global__ __launch_bounds__(256) void k_bwd_cover(Geo g, int64_t dlo, int nChunk, int S, int Sj, int* cover) {
     const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= g.W) return;
-    for (int cls = 0; cls < 4; ++cls) {
-        const int t = cls == 0 ? 0 : cls == 1 ? 1 : cls == 2 ? 3 : 4;
-        int first = -1, count = 0;
+    unsigned short* list = (unsigned short*)(cover + 3 * g.W);
+    for (int cls = 0; cls < 3; ++cls) {
+        const int t = cls == 0 ? 0 : cls == 1 ? 3 : 4;
+        int n = 0;
         for (int j = 0; j < nChunk; ++j) {
+            const ChunkGeo c = chunk_geo(g, dlo, j);
             int64_t lo, hi;
-            type_range(chunk_geo(g, dlo, j), g.r, t, &lo, &hi);
-            if (x >= lo && x < hi) {
-                if (first < 0) first = j;
-                ++count;
+            type_range(c, g.r, t, &lo, &hi);
+            if (x < lo || x >= hi) continue;
+            const int ns = chunk_nseg(c, g.r);
+            // the segment(s) of chunk j whose written range holds column x (<= 2, adjacent)
+            const int64_t rel = x - (c.wlo - g.r) - (cls ? c.d0 : 0);
+            const int sa = (int)(rel >= 0 ? rel / kSeg : -((-rel + kSeg - 1) / kSeg));
+            for (int sg = sa - 1; sg <= sa + 1; ++sg) {
+                if (sg < 0 || sg >= ns) continue;
+                seg_range(c, g.r, sg, t, &lo, &hi);
+                if (x >= lo && x < hi && n < S) list[((size_t)cls * g.W + x) * S + n++] = (unsigned short)(2 * (j % Sj) + (sg & 1));
             }
         }
-        cover[(cls * 2) * g.W + x] = first < 0 ? 0 : first;
-        cover[(cls * 2 + 1) * g.W + x] = count;
+        cover[cls * g.W + x] = n;
     }
 }
 
-// Sum the chunk partials per pixel; out (fp64, [2 sides][4][H][W]): T1, Am|Ac, B|Bp, m'*B.
+// Sum the partial slots per pixel; out (fp64, [2 sides][4][H][W]): T1, Am|Ac, B|Bp, m'*B.
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* acc) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -435,29 +468,24 @@ __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* ac
     if (p >= plane) return;
     const int64_t y = p / g.W, x = p % g.W;
     const int side = blockIdx.y;
+    const unsigned short* list = (const unsigned short*)(a.cover + 3 * g.W);
     double s[3] = {0.0, 0.0, 0.0};
     if (y >= a.ylo && y < a.yhi) {
+#pragma unroll
         for (int q = 0; q < 3; ++q) {
             const int t = 3 * side + q;
-            const int cls = 2 * side + (q == 0 ? 0 : 1);
-            const int first = a.cover[(cls * 2) * g.W + x], n = a.cover[(cls * 2 + 1) * g.W + x];
-            double v = 0.0;
-            for (int i = 0; i < n; ++i) {
-                const int j = first + i;
-                const ChunkGeo c = chunk_geo(g, a.dlo, j);
-                const int ns = chunk_nseg(c, g.r);
-                // the segment(s) of chunk j whose written range holds column x (<= 2, adjacent)
-                const int64_t rel = x - (c.wlo - g.r) - (side ? c.d0 : 0);
-                const int sa = (int)(rel >= 0 ? rel / kSeg : -((-rel + kSeg - 1) / kSeg));
-                for (int sg = sa - 1; sg <= sa + 1; ++sg) {
-                    if (sg < 0 || sg >= ns) continue;
-                    int64_t lo, hi;
-                    seg_range(c, g.r, sg, t, &lo, &hi);
-                    if (x >= lo && x < hi)
-                        v += (double)a.part[((size_t)t * a.S + 2 * (j % a.Sj) + (sg & 1)) * plane + p];
-                }
+            const int cls = side == 0 ? 0 : (q == 0 ? 1 : 2);
+            const int n = a.cover[cls * g.W + x];
+            const unsigned short* sl = list + ((size_t)cls * g.W + x) * a.S;
+            const float* base = a.part + (size_t)t * a.S * plane + p;
+            double v0 = 0.0, v1 = 0.0;
+            int i = 0;
+            for (; i + 1 < n; i += 2) {
+                v0 += (double)base[(size_t)sl[i] * plane];
+                v1 += (double)base[(size_t)sl[i + 1] * plane];
             }
-            s[q] = v;
+            if (i < n) v0 += (double)base[(size_t)sl[i] * plane];
+            s[q] = v0 + v1;
         }
     }
     const Stats& st = side == 0 ? a.sc : a.sp;
@@ -626,7 +654,7 @@ BwdPlan plan_bwd(const Geo& g) {
     const size_t plane = (size_t)g.H * g.W;
     p.part_bytes = (size_t)NTYPE * p.S * plane * sizeof(float);
     p.acc_bytes = 8 * plane * sizeof(double);
-    p.cover_bytes = 8 * (size_t)g.W * sizeof(int);
+    p.cover_bytes = 3 * (size_t)g.W * sizeof(int) + 3 * (size_t)g.W * p.S * sizeof(unsigned short);
     p.prep_bytes = 6 * plane * sizeof(float);
     p.misc_bytes = 2 * kSumBlocks * sizeof(double) + 256;
     return p;
@@ -653,7 +681,8 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     hipLaunchKernelGGL(k_img_blocksum<T>, dim3(kSumBlocks), dim3(256), 0, s, cam, n, bsum);
     hipLaunchKernelGGL(k_img_blocksum<T>, dim3(kSumBlocks), dim3(256), 0, s, proj, n, bsum + kSumBlocks);
     hipLaunchKernelGGL(k_img_shift, dim3(1), dim3(256), 0, s, bsum, kSumBlocks, n, shift);
-    hipLaunchKernelGGL(k_bwd_cover, dim3((unsigned)cdiv(g.W, 256)), dim3(256), 0, s, g, p.dlo, p.nChunk, cover);
+    hipLaunchKernelGGL(k_bwd_cover, dim3((unsigned)cdiv(g.W, 256)), dim3(256), 0, s, g, p.dlo, p.nChunk, p.S, p.Sj,
+                       cover);
     hipLaunchKernelGGL(k_bwd_prep<T>, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, g, cam, proj, sc, sp, shift, prep);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -664,8 +693,9 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     a.S = p.S; a.Sj = p.Sj; a.nChunk = p.nChunk; a.nRG = p.nRG; a.jc = p.jc; a.nsegMax = p.nsegMax;
     a.dlo = p.dlo; a.ylo = p.ylo; a.yhi = p.yhi;
     const int64_t units = (int64_t)p.nChunk * p.nsegMax * p.nRG;
-    const unsigned blocks = (unsigned)(cdiv(units, 8 * kRGT) * 8 * kRGT);
+    const unsigned blocks = (unsigned)(8 * (int64_t)p.nChunk * p.nsegMax * cdiv(p.nRG, 8));
     if (units > 0) {
+        prof_begin(PROF_BWD, s);
         switch (g.k) {
 #define CUSTMA_K(KK) \
     case KK: hipLaunchKernelGGL((k_bwd_sweep<KK>), dim3(blocks), dim3(64), 0, s, g, a); break;
@@ -673,6 +703,7 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
 #undef CUSTMA_K
             default: return hipErrorInvalidValue;
         }
+        prof_end(PROF_BWD, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc);

@@ -10,6 +10,10 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <atomic>
+#include <mutex>
+#include <vector>
+
 #include "common.h"
 #include "sweep.h"
 
@@ -92,6 +96,40 @@ int check_dtype(int32_t dtype) {
 }
 }  // namespace
 
+namespace {
+// Event pairs around the main kernel of every profiled launch (reused across enable calls).
+// Process-wide (the autograd backward runs on its own thread); a bench-only facility.
+struct ProfState {
+    std::atomic<bool> on{false};
+    std::mutex mu;
+    std::vector<hipEvent_t> ev[PROF_NSLOT];  // 2 per launch
+    int n[PROF_NSLOT] = {0, 0};
+};
+ProfState g_prof;
+}  // namespace
+
+void prof_begin(int slot, hipStream_t s) {
+    if (!g_prof.on.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    auto& v = g_prof.ev[slot];
+    const size_t need = 2 * (size_t)(g_prof.n[slot] + 1);
+    while (v.size() < need) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        v.push_back(e);
+    }
+    (void)hipEventRecord(v[2 * g_prof.n[slot]], s);
+}
+
+void prof_end(int slot, hipStream_t s) {
+    if (!g_prof.on.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    auto& v = g_prof.ev[slot];
+    if (v.size() < 2 * (size_t)(g_prof.n[slot] + 1)) return;
+    (void)hipEventRecord(v[2 * g_prof.n[slot] + 1], s);
+    ++g_prof.n[slot];
+}
+
 bool fast_supported(int k) {
     switch (k) {
 #define CUSTMA_K(KK) case KK:
@@ -109,6 +147,34 @@ using namespace custma;
 extern "C" {
 
 int custma_abi_version(void) { return 2; }
+
+int custma_profile_enable(int32_t on) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    g_prof.on = on != 0;
+    g_prof.n[0] = g_prof.n[1] = 0;
+    return CUSTMA_OK;
+}
+
+int custma_profile_mean_ms(int32_t which, float* ms, int32_t* count) {
+    if (which < 0 || which >= PROF_NSLOT || !ms) return fail(CUSTMA_E_ARG, "profile slot %d", which);
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    const int n = g_prof.n[which];
+    if (count) *count = n;
+    *ms = 0.f;
+    if (n == 0) return CUSTMA_OK;
+    auto& v = g_prof.ev[which];
+    int rc = check_hip(hipEventSynchronize(v[2 * n - 1]), "profile sync");
+    if (rc) return rc;
+    double sum = 0.0;
+    for (int i = 0; i < n; ++i) {
+        float t = 0.f;
+        if ((rc = check_hip(hipEventElapsedTime(&t, v[2 * i], v[2 * i + 1]), "profile elapsed"))) return rc;
+        sum += t;
+    }
+    *ms = (float)(sum / n);
+    g_prof.n[which] = 0;
+    return CUSTMA_OK;
+}
 
 const char* custma_last_error(void) { return g_err; }
 

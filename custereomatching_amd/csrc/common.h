@@ -136,4 +136,9 @@ bool backward_supported(const Geo& g);
 hipError_t launch_backward(const float* grad, const float* vol, const void* cam, const void* proj, int dtype,
                            const Geo& g, Stats sc, Stats sp, float* dcam, float* dproj, void* ws, hipStream_t s);
 bool fast_supported(int k);
+
+// Optional HIP-event timing of the main kernel of an op (custma_profile_*): no-ops unless enabled.
+enum ProfSlot { PROF_FWD = 0, PROF_BWD = 1, PROF_NSLOT = 2 };
+void prof_begin(int slot, hipStream_t s);
+void prof_end(int slot, hipStream_t s);
 }  // namespace custma

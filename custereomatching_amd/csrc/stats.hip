@@ -1,62 +1,101 @@
-// Per-pixel patch statistics (one pass over each image, O(H W k^2), tiny
-// next to the volume).  The fp32 mean / sq values replay, in the same order,
-// the arithmetic every reference thread performs for its own patch
-// (custma/src/stereo_matching_kernel.cu:40-54 mean, :56-69 centred squares),
-// so hoisting them per pixel is bit-identical.  The fp64 box sum and
-// fp64-accurate second moment feed the fast sliding-window paths.
+// Per-pixel patch statistics (one pass over each image, tiny next to the volume).
+//
+// mean, sq: the reference's own fp32 values -- the sequential (i, j) sum / k^2 and the
+//   fma chain of centred squares that every reference thread recomputes for its patch
+//   (custma/src/stereo_matching_kernel.cu:40-54 mean, :56-69 centred squares) -- so
+//   hoisting them per pixel is bit-identical.  This k^2-long dependent chain is the
+//   kernel's cost; it runs from an LDS tile, each thread feeding 4 vertically adjacent
+//   pixels from one read of every tile value.
+// box: fp64 patch sum, exact for fp32 inputs within a 2^29 dynamic range, so its value
+//   does not depend on the summation order; formed separably (k-tap row sums in LDS,
+//   then k column taps), 2k fp64 adds per pixel instead of k^2.
+// sqt: fp64-accurate centred second moment box2 - box^2 / k^2 (separable too), rounded
+//   to fp32; only the backward reads it.
 #include "common.h"
 
 namespace custma {
 
 namespace {
-constexpr int TS = 16;  // 16 x 16 pixels per 256-thread workgroup
+constexpr int TX = 16, TY = 64, PR = 4;  // 16 x 64 pixels per 256-thread workgroup, 4 rows per thread
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g, Stats st) {
-    extern __shared__ __attribute__((aligned(16))) float tile[];
-    const int k = g.k, r = g.r, L = TS + 2 * r;
-    const int64_t y0 = (int64_t)blockIdx.y * TS, x0 = (int64_t)blockIdx.x * TS;
-    for (int e = threadIdx.x; e < L * L; e += 256) {
-        const int ty = e / L, tx = e % L;
+    extern __shared__ __attribute__((aligned(16))) double lds_d[];
+    const int k = g.k, r = g.r, LX = TX + 2 * r, LY = TY + 2 * r;
+    double* rs = lds_d;                    // [LY][TX] fp64 k-tap row sums
+    double* rs2 = rs + LY * TX;            // [LY][TX] fp64 k-tap row sums of squares
+    float* tile = (float*)(rs2 + LY * TX);  // [LY][LX] zero-padded image tile
+    const int64_t y0 = (int64_t)blockIdx.y * TY, x0 = (int64_t)blockIdx.x * TX;
+    for (int e = threadIdx.x; e < LY * LX; e += 256) {
+        const int ty = e / LX, tx = e % LX;
         tile[e] = ldpad(img, g.H, g.W, y0 + ty - r, x0 + tx - r);
     }
     __syncthreads();
-    const int ly = threadIdx.x / TS, lx = threadIdx.x % TS;
-    const int64_t y = y0 + ly, x = x0 + lx;
-    if (y >= g.H || x >= g.W) return;
-    const float* t = tile + ly * L + lx;
-    float m = 0.f;
-    double b = 0.0;
-    for (int i = 0; i < k; ++i)
+    for (int e = threadIdx.x; e < LY * TX; e += 256) {
+        const int ty = e / TX, tx = e % TX;
+        const float* t = tile + ty * LX + tx;
+        double a = 0.0, b = 0.0;
         for (int j = 0; j < k; ++j) {
-            const float v = t[i * L + j];
-            m = m + v;
-            b += (double)v;
+            const double v = (double)t[j];
+            a += v;
+            b = fma(v, v, b);
         }
-    m = m / (float)(k * k);
-    const double m64 = b / (double)(k * k);
-    float s = 0.f;
-    double s64 = 0.0;
-    for (int i = 0; i < k; ++i)
+        rs[e] = a;
+        rs2[e] = b;
+    }
+    __syncthreads();
+    const int lx = threadIdx.x % TX, q = threadIdx.x / TX;  // rows PR q .. PR q + PR-1
+    // Each tile value is read once per pass and fed to the PR pixels whose patch holds it;
+    // per pixel the taps still arrive in the reference's (i, j) row-major order.
+    const float* t = tile + (PR * q) * LX + lx;
+    float m[PR], sq[PR];
+#pragma unroll
+    for (int p = 0; p < PR; ++p) { m[p] = 0.f; sq[p] = 0.f; }
+    for (int i2 = 0; i2 < k + PR - 1; ++i2)
         for (int j = 0; j < k; ++j) {
-            const float v = t[i * L + j];
-            const float c = v - m;
-            s = __builtin_fmaf(c, c, s);
-            const double c64 = (double)v - m64;
-            s64 = fma(c64, c64, s64);
+            const float v = t[i2 * LX + j];
+#pragma unroll
+            for (int p = 0; p < PR; ++p)
+                if (i2 - p >= 0 && i2 - p < k) m[p] = m[p] + v;
         }
-    const int64_t p = y * g.W + x;
-    st.mean[p] = m;
-    st.sq[p] = s;
-    st.box[p] = b;
-    st.sqt[p] = (float)s64;
+#pragma unroll
+    for (int p = 0; p < PR; ++p) m[p] = m[p] / (float)(k * k);
+    for (int i2 = 0; i2 < k + PR - 1; ++i2)
+        for (int j = 0; j < k; ++j) {
+            const float v = t[i2 * LX + j];
+#pragma unroll
+            for (int p = 0; p < PR; ++p)
+                if (i2 - p >= 0 && i2 - p < k) {
+                    const float c = v - m[p];
+                    sq[p] = __builtin_fmaf(c, c, sq[p]);
+                }
+        }
+    const int64_t x = x0 + lx;
+    if (x >= g.W) return;
+#pragma unroll
+    for (int p = 0; p < PR; ++p) {
+        const int ly = PR * q + p;
+        const int64_t y = y0 + ly;
+        if (y >= g.H) break;
+        double b = 0.0, b2 = 0.0;
+        for (int i = 0; i < k; ++i) {
+            b += rs[(ly + i) * TX + lx];
+            b2 += rs2[(ly + i) * TX + lx];
+        }
+        const int64_t o = y * g.W + x;
+        st.mean[o] = m[p];
+        st.sq[o] = sq[p];
+        st.box[o] = b;
+        const double c2 = b2 - b * b / (double)(k * k);
+        st.sqt[o] = (float)(c2 > 0.0 ? c2 : 0.0);
+    }
 }
 }  // namespace
 
 hipError_t launch_stats(const void* img, int dtype, const Geo& g, Stats st, hipStream_t s) {
-    const dim3 grid((unsigned)cdiv(g.W, TS), (unsigned)cdiv(g.H, TS));
-    const int L = TS + 2 * g.r;
-    const size_t lds = sizeof(float) * L * L;
+    const dim3 grid((unsigned)cdiv(g.W, TX), (unsigned)cdiv(g.H, TY));
+    const int LX = TX + 2 * g.r, LY = TY + 2 * g.r;
+    const size_t lds = sizeof(double) * 2 * LY * TX + sizeof(float) * LY * LX;
     if (dtype == CUSTMA_F16)
         hipLaunchKernelGGL(k_stats<__half>, grid, dim3(256), lds, s, (const __half*)img, g, st);
     else

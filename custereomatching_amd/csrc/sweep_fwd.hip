@@ -56,7 +56,7 @@ __device__ __forceinline__ void fmac_bc32(float& acc, float a, float b) {
 typedef __attribute__((address_space(3))) volatile double lds_vd;
 
 
-template <int K, int TWT, typename T, bool ARGMAX>
+template <int K, int TWT, typename T, bool ARGMAX, bool DIRECT>
 __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                    Stats sc, Stats sp, float* __restrict__ out, SweepGrid sg,
                                                    DispPartial part) {
@@ -274,6 +274,12 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             voff[m] = ok ? (uint32_t)((m * DO + cb + tid) * 4) : OOB;
         }
     }
+    uint32_t dvoff[TWT];  // DIRECT: this lane's column (window offset d0 + tid) in tile row m
+#pragma unroll
+    for (int m = 0; m < TWT; ++m) {
+        const bool ok = DIRECT && u0 + m < g.WO && d0 + tid < (int64_t)DO;
+        dvoff[m] = ok ? (uint32_t)((m * DO + d0 + tid) * 4) : OOB;
+    }
     // staging index of column c in row m: m*NL + c - d0 - (u0 + m) (full) / m*NL + c - d0
     // (window); with c = voff/4 - m*DO that is voff/4 + m*stgA + stgB
     const int stgA = NL - DO - (window ? 0 : 1), stgB = -(int)d0 - (window ? 0 : (int)u0);
@@ -296,7 +302,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     __syncthreads();  // the loader's first stage
     for (int64_t h = hs; h < h1; ++h) {
         const int buf = (int)((h - hs) & 1);
-        if constexpr (!ARGMAX) {
+        if constexpr (!ARGMAX && !DIRECT) {
             if (h > h0) store_tile(h - 1, buf ^ 1);
         }
 #ifndef CUSTMA_ABL_NOUPDATE  // ablation builds only (scripts/build_ablations.py)
@@ -319,6 +325,10 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
 #pragma unroll
             for (int m = 0; m < TWT; ++m) { mv[m] = mrow[m]; qv[m] = qrow[m]; }
             float* srow = stg + (ARGMAX ? 0 : buf * 16 * NL) + tid;
+            // DIRECT (window layout, one chunk of diagonals): lane tid holds volume column
+            // d0 + tid of the 16 rows u0 .. u0+15, so each m is one 256-byte store from the
+            // registers -- no LDS staging, which leaves room for more workgroups per CU
+            const auto rOutD = make_rsrc(out + ((h - g.h_lo) * g.WO + u0) * g.DO, 0x7FFFFFF0u);
             Unroll<0, TWT>::run([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
                 if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
@@ -329,6 +339,8 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
                 if constexpr (ARGMAX) {
                     srow[m * NL] = (m >= m_lo && m < m_hi) ? c : -FLT_MAX;
+                } else if constexpr (DIRECT) {
+                    if (h >= h0) st_buf(c, rOutD, dvoff[m]);
                 } else {
                     srow[m * NL] = c;
                 }
@@ -376,27 +388,52 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         __syncthreads();
     }
     if constexpr (!ARGMAX) {
-        if (h1 > h0) store_tile(h1 - 1, (int)((h1 - 1 - hs) & 1));
+        if constexpr (!DIRECT) {
+            if (h1 > h0) store_tile(h1 - 1, (int)((h1 - 1 - hs) & 1));
+        }
         __syncthreads();
     }
+}
+
+// DIRECT stores (see the kernel): window layout whose D+1 diagonals fit one chunk of at most
+// 320 lanes.  Off by default: on 2048^2 D=256 k=11 it measured 2.56 ms against 2.34 ms for the
+// LDS-staged sector-owned stores.  CUSTMA_FWD_DIRECT=1 enables it (benchmarking only).
+inline bool use_direct(const Geo& g) {
+    const char* e = getenv("CUSTMA_FWD_DIRECT");
+    return e && atoi(e) != 0 && g.layout == CUSTMA_LAYOUT_WINDOW && g.DO <= 320;
 }
 
 template <int K, typename T>
 hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out,
                     DispPartial* part, hipStream_t s) {
-    const SweepGrid sg = sweep_grid(g, /*owned=*/part == nullptr);
+    const bool direct = part == nullptr && use_direct(g);
+    SweepGrid sg = sweep_grid(g, /*owned=*/part == nullptr && !direct);
+    if (direct) {  // one chunk covering all D+1 diagonals
+        sg.NL = (int)cdiv(g.DO, 64) * 64;
+        sg.S = sg.NL;
+        sg.nChunk = 1;
+        sg.TH = 64;
+        while (sg.TH > 8 && (int64_t)sg.nTile * cdiv(g.HV(), sg.TH) < 4096) sg.TH /= 2;
+        sg.nBand = (int)cdiv(g.HV(), sg.TH);
+    }
     constexpr int R = K / 2, NX = TW + 2 * R;
     const int NL = sg.NL, NO = NX + NL - 1, NS = TW + NL - 1;
     const size_t lds = sizeof(double) * (4 * NO + 2 * 64 + 2 * NS + 2 * 16) +
-                       sizeof(float) * (2 * NS + 2 * 16 + (part ? 1 : 2) * TW * NL);
+                       sizeof(float) * (2 * NS + 2 * 16 + (direct ? 0 : (part ? 1 : 2) * TW * NL));
     const int64_t blocks = sweep_blocks(sg);
     if (part) {
-        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam, proj, g,
-                           sc, sp, out, sg, *part);
+        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam,
+                           proj, g, sc, sp, out, sg, *part);
     } else {
         DispPartial none{};
-        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam, proj, g,
-                           sc, sp, out, sg, none);
+        prof_begin(PROF_FWD, s);
+        if (direct)
+            hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false, true>), dim3((unsigned)blocks), dim3(NL + 64), lds, s,
+                               cam, proj, g, sc, sp, out, sg, none);
+        else
+            hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s,
+                               cam, proj, g, sc, sp, out, sg, none);
+        prof_end(PROF_FWD, s);
     }
     return hipGetLastError();
 }

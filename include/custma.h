@@ -103,6 +103,14 @@ int custma_disparity_band(const void* camera, const void* projector, int32_t dty
                           int64_t* index, float* best, int32_t* n_rechecked, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/* Optional timing of the main kernel of each forward (which = 0: the fast sweep) / backward (which = 1: the
+ * fused gradient sweep) launched on the calling thread while enabled: HIP events recorded on the op's stream
+ * around that one launch (bench.py uses it for the roofline figure over its timed region).
+ * custma_profile_enable(1) starts a new collection; custma_profile_mean_ms synchronises on the last end
+ * event, returns the mean duration and the number of launches, and clears the collection. */
+int custma_profile_enable(int32_t on);
+int custma_profile_mean_ms(int32_t which, float* ms, int32_t* count);
+
 /* First-index argmax over the last axis of a [rows, n] fp32 array (torch.argmax semantics), as the
  * reference's callers do on the volume (examples/verify.py:72, examples/test.py:78-83). */
 int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, float* best, void* stream);

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Forward ablation round trip: stats/parity check then kbench fwd per variant.
+set -o pipefail
+TAG=${1:-ablf}; shift
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 400 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for V in base "$@"; do
+  if [ "$V" = base ]; then L=""; else L=scripts/_abl/$V/libcustma_hip.so; fi
+  CUSTMA_LIB=$L timeout -k 10 300 python scripts/kbench.py --cfg c2_full,c3_win --ops fwd --reps 5 > $O/kb_$V.log 2>&1 || { echo "kbench $V failed"; tail -5 $O/kb_$V.log; exit 1; }
+  echo "== $V"; grep cfg $O/kb_$V.log
+done
+timeout -k 10 300 bash scripts/prof_kernels.sh ${TAG}_prof c3_win fwd | grep -E "stats|sweep"
