@@ -91,6 +91,63 @@ __device__ __forceinline__ float ld_buf<__half>(__amdgpu_buffer_rsrc_t r, uint32
     const unsigned short b = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
     return __half2float(__ushort_as_half(b));
 }
+// Raw bits of one image element (no conversion at the load, so a software pipeline that
+// holds loads in flight across steps does not wait for them where they are issued).
+template <typename T>
+__device__ __forceinline__ uint32_t ld_raw(__amdgpu_buffer_rsrc_t r, uint32_t off);
+template <>
+__device__ __forceinline__ uint32_t ld_raw<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+template <>
+__device__ __forceinline__ uint32_t ld_raw<__half>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+}
+// Software-pipelined loads whose waits the caller places itself (the compiler's vmcnt
+// tracking is conservative at loop headers and would wait for the newest loads).  The
+// compiler does not see these as memory operations: the caller must run
+// `s_waitcnt vmcnt(N)` (asm_vmcnt) before ANY use of the destination, and tie the
+// destination registers to that wait (asm_tie) so no use is scheduled above it.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 make_rsrc_sgpr(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    i32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(a >> 32) & 0xffff);  // stride 0
+    r.z = __builtin_amdgcn_readfirstlane((int32_t)bytes);
+    r.w = 0x00020000;
+    return r;
+}
+template <typename T>
+__device__ __forceinline__ void asm_ld_raw(uint32_t& d, uint32_t off, i32x4 r);
+template <>
+__device__ __forceinline__ void asm_ld_raw<float>(uint32_t& d, uint32_t off, i32x4 r) {
+    asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(d) : "v"(off), "s"(r));
+}
+template <>
+__device__ __forceinline__ void asm_ld_raw<__half>(uint32_t& d, uint32_t off, i32x4 r) {
+    asm volatile("buffer_load_ushort %0, %1, %2, 0 offen" : "=v"(d) : "v"(off), "s"(r));
+}
+__device__ __forceinline__ void asm_ld_f64(double& d, uint32_t off, i32x4 r) {
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(d) : "v"(off), "s"(r));
+}
+template <int N>
+__device__ __forceinline__ void asm_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt field");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <typename V>
+__device__ __forceinline__ void asm_tie(V& v) {
+    asm volatile("" : "+v"(v));
+}
+template <typename T>
+__device__ __forceinline__ double raw_to_f64(uint32_t b);
+template <>
+__device__ __forceinline__ double raw_to_f64<float>(uint32_t b) { return (double)__builtin_bit_cast(float, b); }
+template <>
+__device__ __forceinline__ double raw_to_f64<__half>(uint32_t b) {
+    return (double)__half2float(__ushort_as_half((unsigned short)b));
+}
 __device__ __forceinline__ double ld_buf_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }

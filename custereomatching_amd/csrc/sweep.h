@@ -25,6 +25,64 @@ struct Unroll<NX, NX> {
 
 constexpr int TW = 16;  // camera (own-image) columns per workgroup
 
+// acc += bcast(a, lane L of each 16-lane row) * b, one instruction (DPP row_newbcast on
+// gfx950's fp64 / fp32 FMAC).  Uniform per-step operands (camera pixels, the camera
+// column's patch sum and moment) are held row-replicated in one VGPR (lane i has
+// element i & 15) instead of being re-read from LDS for every product.
+//
+// Hazard: a DPP source VGPR written by a VALU instruction needs 2 wait states before the
+// DPP read (gfx9 "VALU write VGPR -> DPP read").  The compiler cannot see the DPP inside
+// the asm, so every asm block below starts with `s_nop 1`; the batched forms amortise it
+// over several FMAs.
+template <int L>
+__device__ __forceinline__ void fmac_bc64(double& acc, double a, double b) {
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(a), "v"(b), "i"(L));
+}
+template <int L>
+__device__ __forceinline__ void fmac_bc32(float& acc, float a, float b) {
+    asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(a), "v"(b), "i"(L));
+}
+// acc[i] += bcast(a, lane L+i) * pa[i] + bcast(b, lane L+i) * pb[i] for i < 4 (in that order)
+template <int L>
+__device__ __forceinline__ void fmac2_bc64_x4(double& c0, double& c1, double& c2, double& c3, double a, double b,
+                                              double pa0, double pa1, double pa2, double pa3, double pb0,
+                                              double pb1, double pb2, double pb3) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %4, %6 row_newbcast:%14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %4, %7 row_newbcast:%15 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %4, %8 row_newbcast:%16 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %4, %9 row_newbcast:%17 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %5, %10 row_newbcast:%14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %5, %11 row_newbcast:%15 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %5, %12 row_newbcast:%16 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %5, %13 row_newbcast:%17 row_mask:0xf bank_mask:0xf"
+        : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+        : "v"(a), "v"(b), "v"(pa0), "v"(pa1), "v"(pa2), "v"(pa3), "v"(pb0), "v"(pb1), "v"(pb2), "v"(pb3),
+          "i"(L), "i"(L + 1), "i"(L + 2), "i"(L + 3));
+}
+template <int L>
+__device__ __forceinline__ void fmac2_bc64_x2(double& c0, double& c1, double a, double b, double pa0, double pa1,
+                                              double pb0, double pb1) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %2, %4 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %2, %5 row_newbcast:%9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %3, %6 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %3, %7 row_newbcast:%9 row_mask:0xf bank_mask:0xf"
+        : "+v"(c0), "+v"(c1)
+        : "v"(a), "v"(b), "v"(pa0), "v"(pa1), "v"(pb0), "v"(pb1), "i"(L), "i"(L + 1));
+}
+// e += bcast(nb, lane L) * mv;  den2 += bcast(uq, lane L) * qv  (the finalisation's two DPP FMAs)
+template <int L>
+__device__ __forceinline__ void fin_bc(double& e, float& den2, double nb, double mv, float uq, float qv) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %2, %3 row_newbcast:%6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %4, %5 row_newbcast:%6 row_mask:0xf bank_mask:0xf"
+        : "+v"(e), "+v"(den2)
+        : "v"(nb), "v"(mv), "v"(uq), "v"(qv), "i"(L));
+}
+
 // Kernel sizes with a compile-time sweep instantiation (register-resident
 // column sums need a static trip count).  Other odd sizes up to
 // CUSTMA_MAX_KERNEL run on the exact kernel.
@@ -90,6 +148,15 @@ inline SweepGrid sweep_grid(const Geo& g, bool owned = false) {
     sg.nBand = (int)cdiv(g.HV(), sg.TH);
     return sg;
 }
+
+// Wave-independent forward (sweep_wave.hip): one wave per (row band, column tile, chunk of
+// 64 diagonals).
+struct WaveGrid {
+    int nChunk, nTile, nBand, TH;
+};
+WaveGrid wave_grid(const Geo& g);
+hipError_t launch_fwd_lds(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
+                          float* out, hipStream_t s);
 
 inline int64_t sweep_blocks(const SweepGrid& sg) { return (int64_t)sg.nBand * sg.nTile * sg.nChunk; }
 

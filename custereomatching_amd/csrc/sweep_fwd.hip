@@ -41,19 +41,10 @@ namespace custma {
 
 namespace {
 
-// acc += bcast(a, lane L of each 16-lane row) * b, one instruction (DPP row_newbcast on
-// gfx950's fp64 / fp32 FMAC).  Uniform per-step operands (camera pixels, the camera
-// column's patch sum and moment) are held row-replicated in one VGPR (lane i has
-// element i & 15) instead of being re-read from LDS for every product.
-template <int L>
-__device__ __forceinline__ void fmac_bc64(double& acc, double a, double b) {
-    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(a), "v"(b), "i"(L));
-}
-template <int L>
-__device__ __forceinline__ void fmac_bc32(float& acc, float a, float b) {
-    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(a), "v"(b), "i"(L));
-}
 typedef __attribute__((address_space(3))) volatile double lds_vd;
+#ifndef CUSTMA_FWD_NST
+#define CUSTMA_FWD_NST 2  // loader register stages (x loads per step <= 63 + one step)
+#endif
 
 
 template <int K, int TWT, typename T, bool ARGMAX, bool DIRECT>
@@ -64,14 +55,18 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     static_assert(TWT == 16 && NX <= 32, "row-broadcast layout assumes 16 own columns and <= 32 taps");
     constexpr int NL_MAX = 320, LO = (NX + NL_MAX - 1 + 63) / 64, LS = (TWT + NL_MAX - 1 + 63) / 64;
     const int NL = sg.NL, NO = NX + NL - 1, NS = TWT + NL - 1;
+    // LDS rows are padded to whole loader-lane chunks (OP = 64 LO, SP = 64 LS), so the loader
+    // writes every lane of every chunk unconditionally (the padding takes zeros / ignored
+    // values): its step is straight-line code, which keeps three steps of loads in flight
+    constexpr int OP = 64 * LO, SP = 64 * LS;
     extern __shared__ __attribute__((aligned(16))) double ldsd[];
-    double* ringO = ldsd;                  // [2 buf][2 enter/leave][NO] projector rows
-    double* ringU = ringO + 4 * NO;        // [2 buf][64]: +c of the entering row, -c of the leaving row
-    double* rsM = ringU + 2 * 64;          // [2][NS]  projector fp64 patch means
-    double* usB = rsM + 2 * NS;            // [2][16]  -(camera fp64 patch sums)
-    float* rsQ = (float*)(usB + 2 * 16);   // [2][NS]  projector ey2
-    float* usQ = rsQ + 2 * NS;             // [2][16]  camera ex2
-    float* stg = usQ + 2 * 16;             // [2][16][NL] cost tile staging (ARGMAX: [16][NL] reduction)
+    double* ringO = ldsd;                  // [2 buf][2 enter/leave][OP] projector rows
+    double* ringU = ringO + 4 * OP;        // [2 buf][64]: +c of the entering row, -c of the leaving row
+    double* rsM = ringU + 2 * 64;          // [2][SP]  projector fp64 patch means
+    double* usB = rsM + 2 * SP;            // [2][64]  -(camera fp64 patch sums) (lanes 0-15)
+    float* rsQ = (float*)(usB + 2 * 64);   // [2][SP]  projector ey2
+    float* usQ = rsQ + 2 * SP;             // [2][64]  camera ex2 (lanes 0-15)
+    float* stg = usQ + 2 * 64;             // [2][16][NL] cost tile staging (ARGMAX: [16][NL] reduction)
 
     const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
     const int chunk = (int)(bid % sg.nChunk);
@@ -105,7 +100,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         };
         auto row_rsrc = [&](const void* base, int64_t row, int esz, bool ok) {
             ok = ok && row >= 0 && row < g.H;
-            return make_rsrc((const char*)base + (ok ? row : 0) * g.W * esz, ok ? (uint32_t)(g.W * esz) : 0u);
+            return make_rsrc_sgpr((const char*)base + (ok ? row : 0) * g.W * esz, ok ? (uint32_t)(g.W * esz) : 0u);
         };
         uint32_t vO[LO], vSd[LS], vSf[LS];
         const uint32_t vUe = colOff(li < NX, xU0 + li, sizeof(T));
@@ -118,8 +113,12 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             vSd[j] = colOff(li + 64 * j < NS, oS + li + 64 * j, 8);
             vSf[j] = colOff(li + 64 * j < NS, oS + li + 64 * j, 4);
         }
+        // Raw bits only: nothing consumes a load in the step that issues it, and every load is
+        // unconditional (unused lanes / chunks carry the out-of-range offset), so the loads of
+        // three steps stay in flight (the compiler's vmcnt waits only for the oldest stage).
+        constexpr int NST = CUSTMA_FWD_NST;
         struct Stage {
-            float ue, ul, oe[LO], ol[LO], q[LS], uq;
+            uint32_t ue, ul, oe[LO], ol[LO], q[LS], uq;
             double m[LS], ub;
         };
         // step t adds image row t+R and removes row t-R-1 (once it was added: rows from
@@ -128,71 +127,89 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             const bool rem = t > h0;
             const auto rCe = row_rsrc(cam, t + R, sizeof(T), true), rCl = row_rsrc(cam, t - R - 1, sizeof(T), rem);
             const auto rPe = row_rsrc(proj, t + R, sizeof(T), true), rPl = row_rsrc(proj, t - R - 1, sizeof(T), rem);
-            p.ue = ld_buf<T>(rCe, vUe);
-            p.ul = ld_buf<T>(rCl, vUl);
+            asm_ld_raw<T>(p.ue, vUe, rCe);
+            asm_ld_raw<T>(p.ul, vUl, rCl);
 #pragma unroll
             for (int j = 0; j < LO; ++j) {
-                if (j > 0 && 64 * j >= NO) break;
-                p.oe[j] = ld_buf<T>(rPe, vO[j]);
-                p.ol[j] = ld_buf<T>(rPl, vO[j]);
+                asm_ld_raw<T>(p.oe[j], vO[j], rPe);
+                asm_ld_raw<T>(p.ol[j], vO[j], rPl);
             }
             const bool st = t >= h0 && t < h1;
             const auto rPB = row_rsrc(sp.box, t, 8, st), rPS = row_rsrc(sp.sq, t, 4, st);
             const auto rCB = row_rsrc(sc.box, t, 8, st), rCS = row_rsrc(sc.sq, t, 4, st);
 #pragma unroll
             for (int j = 0; j < LS; ++j) {
-                if (j > 0 && 64 * j >= NS) break;
-                p.m[j] = ld_buf_f64(rPB, vSd[j]);
-                p.q[j] = ld_buf<float>(rPS, vSf[j]);
+                asm_ld_f64(p.m[j], vSd[j], rPB);
+                asm_ld_raw<float>(p.q[j], vSf[j], rPS);
             }
-            p.ub = ld_buf_f64(rCB, vUSd);
-            p.uq = ld_buf<float>(rCS, vUSf);
+            asm_ld_f64(p.ub, vUSd, rCB);
+            asm_ld_raw<float>(p.uq, vUSf, rCS);
+        };
+        constexpr int kLoadsPerStep = 4 + 2 * LO + 2 * LS;
+        // the oldest stage has landed once at most (NST - 1) steps of loads are outstanding
+        auto wait_oldest = [&](Stage& p) {
+            asm_vmcnt<kLoadsPerStep * (NST - 1)>();
+            asm_tie(p.ue);
+            asm_tie(p.ul);
+            asm_tie(p.uq);
+            asm_tie(p.ub);
+#pragma unroll
+            for (int j = 0; j < LO; ++j) { asm_tie(p.oe[j]); asm_tie(p.ol[j]); }
+#pragma unroll
+            for (int j = 0; j < LS; ++j) { asm_tie(p.m[j]); asm_tie(p.q[j]); }
         };
         auto store_step = [&](int b, const Stage& p) {
-            ringU[b * 64 + li] = li < 32 ? (double)p.ue : -(double)p.ul;  // 0 past NX
+            ringU[b * 64 + li] = li < 32 ? raw_to_f64<T>(p.ue) : -raw_to_f64<T>(p.ul);  // 0 past NX
 #pragma unroll
-            for (int j = 0; j < LO; ++j)
-                if (64 * j < NO && li + 64 * j < NO) {
-                    ringO[(2 * b) * NO + li + 64 * j] = (double)p.oe[j];
-                    ringO[(2 * b + 1) * NO + li + 64 * j] = (double)p.ol[j];
-                }
-#pragma unroll
-            for (int j = 0; j < LS; ++j)
-                if (64 * j < NS && li + 64 * j < NS) {
-                    rsM[b * NS + li + 64 * j] = p.m[j] * rk2;
-                    rsQ[b * NS + li + 64 * j] = p.q[j];
-                }
-            if (li < 16) { usB[b * 16 + li] = -p.ub; usQ[b * 16 + li] = p.uq; }
-        };
-        // three register stages: the loads of step t are issued at step t-3, so two full
-        // steps pass before the loader waits for them (a single step of slack left every
-        // step waiting out a global-load round trip)
-        Stage st[3];
-        load_step(hs, st[0]);
-        store_step(0, st[0]);
-        load_step(hs + 1, st[1]);
-        load_step(hs + 2, st[2]);
-        load_step(hs + 3, st[0]);
-        __syncthreads();
-        // iteration i = t - hs stores step t+1 (stage (i+1)%3) and refills that stage with
-        // step t+4; the barrier count matches the compute waves' exactly
-        auto step = [&](auto kc, int64_t t) {
-            constexpr int k = decltype(kc)::value;  // == (t - hs + 1) % 3
-            const int i = (int)(t - hs);
-            store_step((i + 1) & 1, st[k]);
-            load_step(t + 4, st[k]);  // past the band's end: harmless, unused
-            if constexpr (ARGMAX) {
-                if (t >= h0) __syncthreads();
+            for (int j = 0; j < LO; ++j) {
+                ringO[(2 * b) * OP + li + 64 * j] = raw_to_f64<T>(p.oe[j]);
+                ringO[(2 * b + 1) * OP + li + 64 * j] = raw_to_f64<T>(p.ol[j]);
             }
-            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < LS; ++j) {
+                rsM[b * SP + li + 64 * j] = p.m[j] * rk2;
+                rsQ[b * SP + li + 64 * j] = __builtin_bit_cast(float, p.q[j]);
+            }
+            usB[b * 64 + li] = -p.ub;
+            usQ[b * 64 + li] = __builtin_bit_cast(float, p.uq);
         };
-        for (int64_t t = hs;; t += 3) {
-            if (t >= h1) break;
-            step(std::integral_constant<int, 1>{}, t);
-            if (t + 1 >= h1) break;
-            step(std::integral_constant<int, 2>{}, t + 1);
-            if (t + 2 >= h1) break;
-            step(std::integral_constant<int, 0>{}, t + 2);
+        // NST register stages: the loads of step hs+s are issued in iteration s-NST and
+        // stored to LDS in iteration s (vmcnt counts at most 63 loads in flight: NST x the
+        // loads of one step must stay below that, or the compiler waits for all of them).  The
+        // warm-up iterations (s < 0) run the same loop body with the LDS store and the
+        // barrier skipped: no loads are issued outside the loop, so the loop-header state
+        // the compiler's vmcnt tracking sees is the loop's own (a peeled prologue with a
+        // different register assignment made it wait for the newest loads every iteration).
+        // Iteration s >= 0 ends with barrier #s: compute step hs+s-1 ends with it (#0: the
+        // first stage), and the loader issues as many barriers as the compute waves.
+        Stage st[NST];
+        const int n = (int)(h1 - hs);
+        auto step = [&](auto kc, int s) {
+            constexpr int k = decltype(kc)::value;  // == (s + NST) % NST
+            if (s >= 0) {
+                wait_oldest(st[k]);
+                store_step(s & 1, st[k]);
+            }
+            load_step(hs + s + NST, st[k]);  // past the band's end: harmless, unused
+            if (s >= 0) {
+                if constexpr (ARGMAX) {
+                    if (s >= 1 && hs + s - 1 >= h0) __syncthreads();
+                }
+                __syncthreads();
+            }
+        };
+        // opaque start: the compiler must not peel the warm-up iterations into a prologue
+        int s_first = -NST;
+        asm volatile("" : "+s"(s_first));
+        for (int s = s_first;; s += NST) {
+            bool done = false;
+            Unroll<0, NST>::run([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                if (done) return;
+                step(kc, s + k);
+                done = s + k >= n;
+            });
+            if (done) break;
         }
         if constexpr (!ARGMAX) __syncthreads();  // the compute waves' final store phase
         return;
@@ -217,8 +234,8 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         const double cb0 = ringU[b * 64 + 32 + r16], cb1 = ringU[b * 64 + 48 + r16];  // negated
         // volatile: keeps these as single ds_read_b64 (2 LDS cycles per wave-instruction)
         // instead of pairs merged into ds_read2_b64 (8 cycles, half the bandwidth)
-        const lds_vd* oa = (const lds_vd*)(ringO + (2 * b) * NO + tid);
-        const lds_vd* ob = (const lds_vd*)(ringO + (2 * b + 1) * NO + tid);
+        const lds_vd* oa = (const lds_vd*)(ringO + (2 * b) * OP + tid);
+        const lds_vd* ob = (const lds_vd*)(ringO + (2 * b + 1) * OP + tid);
         // batches of B columns, double-buffered: batch b+1's reads are in flight while
         // batch b's FMAs issue (an asm statement is a scheduling boundary)
         constexpr int B = 4, NB = (NX + B - 1) / B;
@@ -316,10 +333,10 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
 #pragma unroll
             for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
-            const lds_vd* mrow = (const lds_vd*)(rsM + buf * NS + tid);
-            const float* qrow = rsQ + buf * NS + tid;
-            const double nb = usB[buf * 16 + r16];  // -(camera patch sum) of column r16
-            const float uq = usQ[buf * 16 + r16];   // camera ex2 of column r16
+            const lds_vd* mrow = (const lds_vd*)(rsM + buf * SP + tid);
+            const float* qrow = rsQ + buf * SP + tid;
+            const double nb = usB[buf * 64 + r16];  // -(camera patch sum) of column r16
+            const float uq = usQ[buf * 64 + r16];   // camera ex2 of column r16
             double mv[TWT];
             float qv[TWT];
 #pragma unroll
@@ -417,9 +434,10 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
         sg.nBand = (int)cdiv(g.HV(), sg.TH);
     }
     constexpr int R = K / 2, NX = TW + 2 * R;
-    const int NL = sg.NL, NO = NX + NL - 1, NS = TW + NL - 1;
-    const size_t lds = sizeof(double) * (4 * NO + 2 * 64 + 2 * NS + 2 * 16) +
-                       sizeof(float) * (2 * NS + 2 * 16 + (direct ? 0 : (part ? 1 : 2) * TW * NL));
+    constexpr int NL_MAX = 320, OP = 64 * ((NX + NL_MAX - 1 + 63) / 64), SP = 64 * ((TW + NL_MAX - 1 + 63) / 64);
+    const int NL = sg.NL;
+    const size_t lds = sizeof(double) * (4 * OP + 2 * 64 + 2 * SP + 2 * 64) +
+                       sizeof(float) * (2 * SP + 2 * 64 + (direct ? 0 : (part ? 1 : 2) * TW * NL));
     const int64_t blocks = sweep_blocks(sg);
     if (part) {
         hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam,
@@ -452,8 +470,8 @@ hipError_t dispatch(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
 
 }  // namespace
 
-hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
-                           float* out, hipStream_t s) {
+hipError_t launch_fwd_lds(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
+                          float* out, hipStream_t s) {
     if (dtype == CUSTMA_F16)
         return dispatch((const __half*)cam, (const __half*)proj, g, sc, sp, out, nullptr, s);
     return dispatch((const float*)cam, (const float*)proj, g, sc, sp, out, nullptr, s);

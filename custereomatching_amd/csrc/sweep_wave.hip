@@ -1,0 +1,293 @@
+// Fast forward, wave-independent form: the default volume-writing sweep.
+//
+// Same arithmetic as k_sweep_fwd (sweep_fwd.hip; reference: custma/src/
+// stereo_matching_kernel.cu:39-71): per disparity diagonal delta = d - w the
+// patch sums of c * p slide down the rows and across the columns in fp64
+// (fp32 x fp32 products are exact there), the mean correction uses the fp64
+// patch sums, and the denominator the reference's own fp32 moments:
+//     cost = (float)(S + eps - boxc * boxp / k^2) * rsq(fma(ex2, ey2, eps)).
+//
+// Work unit = ONE wave: 64 consecutive diagonals (lane l: delta = d0 + l) x 16
+// camera columns (u0 .. u0+15) x a band of TH rows.  Unlike k_sweep_fwd there
+// is no loader wave, no workgroup barrier and no output staging: every wave
+// loads its own image rows and statistics (14 buffer loads per row step, two
+// steps in flight, issued as inline asm with hand-counted `s_waitcnt vmcnt`
+// -- the compiler's own tracking drains the pipeline at the loop header), puts
+// the two projector row segments and the projector statistics in a 3.5 KB
+// wave-private LDS slice (the sliding-window reads need them there), keeps the
+// camera values row-replicated in registers (DPP row_newbcast operands), and
+// stores the 16 volume rows of a step straight from registers: lane l writes
+// volume column d0 + l (window layout) / u0 + m + d0 + l (full layout), so
+// each store instruction is 256 contiguous bytes of one volume row.
+//
+// Per voxel: 2(16+2r)/16 fp64 FMAs + as many ds_read_b64 (row update), 2 fp64
+// adds (column slide), 1 fp64 FMA + cvt (mean correction), fp32 fma + rsq + mul.
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "common.h"
+#include "sweep.h"
+
+namespace custma {
+
+namespace {
+
+typedef __attribute__((address_space(3))) volatile double lds_vd;
+typedef __attribute__((address_space(3))) volatile float lds_vf;
+
+constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
+
+template <int K, typename T, bool FULL_EDGE>
+__device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
+                                          const Stats& sc, const Stats& sp, float* __restrict__ out,
+                                          int64_t u0, int64_t h0, int64_t h1, int64_t d0,
+                                          double* rowE, double* rowL, double* sM, float* sQ) {
+    constexpr int R = K / 2, NX = TW + 2 * R;
+    static_assert(NX + 63 <= kRowP && NX <= 32, "row segment fits the LDS slice and two broadcast registers");
+    constexpr uint32_t OOB = 0x80000000u;
+    const int l = threadIdx.x, r16 = l & 15;
+    const int64_t hs = h0 - 2 * R;  // 2R warm-up steps fill the column sums
+    const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
+    const double rk2 = 1.0 / (double)(K * K);
+
+    // ---- per-lane column byte offsets (out of the image -> OOB -> 0: the reference's zero
+    // padding, stereo_matching_kernel.cu:6-12); rows are selected by the descriptors ----
+    auto colOff = [&](bool have, int64_t x, int esz) -> uint32_t {
+        return (have && x >= 0 && x < g.W) ? (uint32_t)(x * esz) : OOB;
+    };
+    const int64_t xO0 = u0 - R + d0, oS = u0 + d0;
+    const uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 63, xO0 + 64 + l, sizeof(T));
+    const uint32_t vC0 = colOff(true, u0 - R + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R + 16 + r16, sizeof(T));
+    const uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 63, oS + 64 + l, 8);
+    const uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 63, oS + 64 + l, 4);
+    const uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
+    auto row_rsrc = [&](const void* base, int64_t row, int esz, bool ok) {
+        ok = ok && row >= 0 && row < g.H;
+        return make_rsrc_sgpr((const char*)base + (ok ? row : 0) * g.W * esz, ok ? (uint32_t)(g.W * esz) : 0u);
+    };
+
+    struct Stage {
+        uint32_t pe0, pe1, pl0, pl1, ce0, ce1, cl0, cl1, q0, q1, uq;
+        double m0, m1, ub;
+    };
+    constexpr int kLoads = 14;
+    // step t adds image row t+R and removes row t-R-1 (rows from h0-R on were added, so the
+    // first removal is at t = h0+1); statistics of row t (only for t in [h0, h1))
+    auto load_step = [&](int64_t t, Stage& p) {
+        const bool rem = t > h0;
+        const auto rCe = row_rsrc(cam, t + R, sizeof(T), true), rCl = row_rsrc(cam, t - R - 1, sizeof(T), rem);
+        const auto rPe = row_rsrc(proj, t + R, sizeof(T), true), rPl = row_rsrc(proj, t - R - 1, sizeof(T), rem);
+        asm_ld_raw<T>(p.pe0, vP0, rPe);
+        asm_ld_raw<T>(p.pe1, vP1, rPe);
+        asm_ld_raw<T>(p.pl0, vP0, rPl);
+        asm_ld_raw<T>(p.pl1, vP1, rPl);
+        asm_ld_raw<T>(p.ce0, vC0, rCe);
+        asm_ld_raw<T>(p.ce1, vC1, rCe);
+        asm_ld_raw<T>(p.cl0, vC0, rCl);
+        asm_ld_raw<T>(p.cl1, vC1, rCl);
+        const bool st = t >= h0 && t < h1;
+        const auto rPB = row_rsrc(sp.box, t, 8, st), rPS = row_rsrc(sp.sq, t, 4, st);
+        const auto rCB = row_rsrc(sc.box, t, 8, st), rCS = row_rsrc(sc.sq, t, 4, st);
+        asm_ld_f64(p.m0, vM0, rPB);
+        asm_ld_f64(p.m1, vM1, rPB);
+        asm_ld_raw<float>(p.q0, vQ0, rPS);
+        asm_ld_raw<float>(p.q1, vQ1, rPS);
+        asm_ld_f64(p.ub, vUB, rCB);
+        asm_ld_raw<float>(p.uq, vUQ, rCS);
+    };
+    auto tie = [&](Stage& p) {
+        asm_tie(p.pe0); asm_tie(p.pe1); asm_tie(p.pl0); asm_tie(p.pl1);
+        asm_tie(p.ce0); asm_tie(p.ce1); asm_tie(p.cl0); asm_tie(p.cl1);
+        asm_tie(p.q0); asm_tie(p.q1); asm_tie(p.uq); asm_tie(p.m0); asm_tie(p.m1); asm_tie(p.ub);
+    };
+
+    // ---- output addressing: one descriptor per step (volume rows (h, u0 .. u0+15), clipped
+    // to the valid camera columns), the tile row m in soffset, the column in voffset ----
+    const int64_t DO = g.DO;
+    const int64_t a0 = window ? d0 + l : u0 + d0 + l;  // volume column of tile row 0
+    uint32_t vOut = OOB;                              // constant per lane unless FULL_EDGE
+    if (window) vOut = (d0 + l <= g.D) ? (uint32_t)(a0 * 4) : OOB;
+    else if (!FULL_EDGE) vOut = (uint32_t)(a0 * 4);  // interior chunk: every voxel valid
+    const int64_t nrow = min((int64_t)TW, g.WO - u0);
+    const uint32_t tile_bytes = (uint32_t)(nrow * DO * 4);
+    const int sstep = (int)((DO + (window ? 0 : 1)) * 4);  // soffset per tile row
+
+    double col[NX];
+#pragma unroll
+    for (int x = 0; x < NX; ++x) col[x] = 0.0;
+
+    // The loads of step t are issued at the end of step t-2.  The first two issues happen in
+    // two warm-up iterations of the loop itself (t = hs-2, hs-1: loads only), not in a
+    // prologue: the compiler believes an asm load's destination is written when the asm
+    // issues, so a peeled prologue with another register assignment would be joined to the
+    // loop by register copies -- reads of registers whose loads are still in flight.
+    Stage st[2];
+    auto compute = [&](Stage& p, int64_t t) {
+        // loads(t) were issued at the end of step t-2; after them: the stores of step t-1
+        // (16, from step h0 on) and the loads of step t+1
+        if (t - 1 >= h0) asm_vmcnt<kLoads + TW>();
+        else asm_vmcnt<kLoads>();
+        tie(p);
+        rowE[l] = raw_to_f64<T>(p.pe0);
+        rowE[64 + l] = raw_to_f64<T>(p.pe1);
+        rowL[l] = raw_to_f64<T>(p.pl0);
+        rowL[64 + l] = raw_to_f64<T>(p.pl1);
+        sM[l] = p.m0 * rk2;
+        sM[64 + l] = p.m1 * rk2;
+        sQ[l] = __builtin_bit_cast(float, p.q0);
+        sQ[64 + l] = __builtin_bit_cast(float, p.q1);
+        const double ca0 = raw_to_f64<T>(p.ce0), ca1 = raw_to_f64<T>(p.ce1);
+        const double cb0 = -raw_to_f64<T>(p.cl0), cb1 = -raw_to_f64<T>(p.cl1);
+        const double nb = -p.ub;                           // -(camera patch sum) of column r16
+        const float uq = __builtin_bit_cast(float, p.uq);  // camera ex2 of column r16
+
+        // ---- col[x] += c(enter, x) p(enter, x + delta) - c(leave, x) p(leave, x + delta) ----
+        {
+            const lds_vd* oa = (const lds_vd*)(rowE + l);
+            const lds_vd* ob = (const lds_vd*)(rowL + l);
+            constexpr int B = 4, NB = (NX + B - 1) / B;
+            double pa[2][B], pb[2][B];
+            auto fetch = [&](auto bc) {
+                constexpr int bb = decltype(bc)::value, x0 = bb * B;
+                constexpr int nb_ = NX - x0 < B ? NX - x0 : B;
+                Unroll<0, nb_>::run([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    pa[bb & 1][i] = oa[x0 + i];
+                    pb[bb & 1][i] = ob[x0 + i];
+                });
+            };
+            fetch(std::integral_constant<int, 0>{});
+            Unroll<0, NB>::run([&](auto bc) {
+                constexpr int bb = decltype(bc)::value, x0 = bb * B;
+                constexpr int nb_ = NX - x0 < B ? NX - x0 : B;
+                if constexpr (bb + 1 < NB) fetch(std::integral_constant<int, bb + 1>{});
+                const double a = x0 < 16 ? ca0 : ca1, b = x0 < 16 ? cb0 : cb1;  // x0 % 4 == 0
+                const double* qa = pa[bb & 1];
+                const double* qb = pb[bb & 1];
+                if constexpr (nb_ == 4) {
+                    fmac2_bc64_x4<(x0 & 15)>(col[x0], col[x0 + 1], col[x0 + 2], col[x0 + 3], a, b, qa[0], qa[1],
+                                             qa[2], qa[3], qb[0], qb[1], qb[2], qb[3]);
+                } else if constexpr (nb_ == 2) {
+                    fmac2_bc64_x2<(x0 & 15)>(col[x0], col[x0 + 1], a, b, qa[0], qa[1], qb[0], qb[1]);
+                } else {
+                    Unroll<0, nb_>::run([&](auto ic) {
+                        constexpr int i = decltype(ic)::value, x = x0 + i;
+                        fmac_bc64<(x & 15)>(col[x], a, qa[i]);
+                        fmac_bc64<(x & 15)>(col[x], b, qb[i]);
+                    });
+                }
+            });
+        }
+
+        if (t >= h0) {
+            const auto rOut = make_rsrc(out + ((t - g.h_lo) * g.WO + u0) * DO, tile_bytes);
+            double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
+#pragma unroll
+            for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
+            const lds_vd* mrow = (const lds_vd*)(sM + l);
+            const lds_vf* qrow = (const lds_vf*)(sQ + l);
+            Unroll<0, TW>::run([&](auto mc) {
+                constexpr int m = decltype(mc)::value;
+                if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
+                double e = s;
+                float den2 = kEps;
+                // E + eps = S + eps - box_c * mean_p;  ex2 * ey2 + eps
+                fin_bc<m>(e, den2, nb, mrow[m], uq, qrow[m]);
+                const float c = (float)e * __builtin_amdgcn_rsqf(den2);
+                uint32_t vo = vOut, so = (uint32_t)(m * sstep);
+                if constexpr (FULL_EDGE) {  // per-row mask; the whole offset in voffset
+                    vo = ((uint64_t)(a0 + m) < (uint64_t)g.W) ? (uint32_t)((a0 + m + m * DO) * 4) : OOB;
+                    so = 0;
+                }
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, so,
+                                                      CUSTMA_STORE_AUX);
+            });
+        }
+    };
+    auto step = [&](auto kc, int64_t t) {
+        Stage& p = st[decltype(kc)::value];
+        if (t >= hs) compute(p, t);
+        load_step(t + 2, p);  // past the band's end: harmless (rows out of range read zeros)
+    };
+    int64_t t_first = hs - 2;  // opaque: the warm-up iterations must not be peeled
+    asm volatile("" : "+s"(t_first));
+    for (int64_t t = t_first;; t += 2) {
+        step(std::integral_constant<int, 0>{}, t);
+        if (t + 1 >= h1) break;
+        step(std::integral_constant<int, 1>{}, t + 1);
+        if (t + 2 >= h1) break;
+    }
+    asm_vmcnt<0>();  // every wave drains its own loads before it ends
+}
+
+template <int K, typename T>
+__global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
+                                                 Stats sc, Stats sp, float* __restrict__ out, WaveGrid wg) {
+    __shared__ __attribute__((aligned(16))) double rowE[kRowP], rowL[kRowP], sM[kRowP];
+    __shared__ __attribute__((aligned(16))) float sQ[kRowP];
+    const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int chunk = (int)(bid % wg.nChunk);
+    const int64_t rest = bid / wg.nChunk;
+    const int wt = (int)(rest % wg.nTile);
+    const int band = (int)(rest / wg.nTile);
+    const int64_t u0 = (int64_t)wt * TW;
+    const int64_t h0 = g.h_lo + (int64_t)band * wg.TH, h1 = min(g.h_hi, h0 + wg.TH);
+    const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
+    const int64_t dlo = window ? 0 : -(u0 + TW - 1);
+    const int64_t d0 = dlo + (int64_t)chunk * 64;
+    // full layout: a chunk with a voxel outside [0, W) for some tile row needs per-row masks
+    const bool edge = !window && (u0 + d0 < 0 || u0 + TW - 1 + d0 + 63 >= g.W);
+    if (edge)
+        wave_body<K, T, true>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ);
+    else
+        wave_body<K, T, false>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ);
+}
+
+template <int K, typename T>
+hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out, hipStream_t s) {
+    const WaveGrid wg = wave_grid(g);
+    const int64_t blocks = (int64_t)wg.nBand * wg.nTile * wg.nChunk;
+    prof_begin(PROF_FWD, s);
+    hipLaunchKernelGGL((k_fwd_wave<K, T>), dim3((unsigned)blocks), dim3(64), 0, s, cam, proj, g, sc, sp, out, wg);
+    prof_end(PROF_FWD, s);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t dispatch(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out, hipStream_t s) {
+    switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: return launch_k<KK, T>(cam, proj, g, sc, sp, out, s);
+        CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+WaveGrid wave_grid(const Geo& g) {
+    WaveGrid wg;
+    const int64_t nd = g.layout == CUSTMA_LAYOUT_WINDOW ? (int64_t)g.D + 1 : g.W + TW - 1;
+    wg.nChunk = (int)cdiv(nd, 64);
+    wg.nTile = (int)cdiv(g.WO, TW);
+    // tuning override (benchmarking only): CUSTMA_WAVE_TH
+    const char* e = getenv("CUSTMA_WAVE_TH");
+    wg.TH = e && atoi(e) > 0 ? atoi(e) : 64;
+    // keep >= ~8 waves per SIMD on small problems
+    while (wg.TH > 8 && (int64_t)wg.nTile * wg.nChunk * cdiv(g.HV(), wg.TH) < 8192) wg.TH /= 2;
+    wg.nBand = (int)cdiv(g.HV(), wg.TH);
+    return wg;
+}
+
+hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
+                           float* out, hipStream_t s) {
+    // CUSTMA_FWD_LDS=1: the workgroup (loader wave + LDS-staged stores) form, for comparison
+    const char* e = getenv("CUSTMA_FWD_LDS");
+    if (e && atoi(e) != 0) return launch_fwd_lds(cam, proj, dtype, g, sc, sp, out, s);
+    if (dtype == CUSTMA_F16) return dispatch((const __half*)cam, (const __half*)proj, g, sc, sp, out, s);
+    return dispatch((const float*)cam, (const float*)proj, g, sc, sp, out, s);
+}
+
+}  // namespace custma

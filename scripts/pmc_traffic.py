@@ -58,6 +58,6 @@ for kern in ("k_bwd_sweep", "k_sweep_fwd"):
                            "source": "scripts/micro/fetch_calib.hip, 1 GiB streamed per kernel"},
            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
            "note": "fabric-side request counters (TCC_EA0): Infinity-Cache hits are counted as well"}
-    p = os.path.join(root, "profiles", f"pmc_{kern}_c2_{layout}.json")
+    p = os.path.join(out, f"pmc_{kern}_c2_{layout}.json")  # copied into profiles/ by hand
     json.dump(res, open(p, "w"), indent=1)
     print(kern, json.dumps(res))
