@@ -247,12 +247,12 @@ def main():
     fwd_bytes = nvox_rank * 4 + img
     bwd_bytes = 2 * nvox_rank * 4 + img + img
     kern = {
-        "k_sweep_fwd": {"avg_launch_ms": round(fwd_kms, 4), "launches": n_fk, "algorithmic_bytes": fwd_bytes,
+        "k_fwd_wave": {"avg_launch_ms": round(fwd_kms, 4), "launches": n_fk, "algorithmic_bytes": fwd_bytes,
                         "achieved_GBps": round(fwd_bytes / (fwd_kms * 1e-3) / 1e9, 1) if fwd_kms else None},
         "k_bwd_sweep": {"avg_launch_ms": round(bwd_kms, 4), "launches": n_bk, "algorithmic_bytes": bwd_bytes,
                         "achieved_GBps": round(bwd_bytes / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None},
     }
-    dom = "k_bwd_sweep" if bwd_kms >= fwd_kms else "k_sweep_fwd"
+    dom = "k_bwd_sweep" if bwd_kms >= fwd_kms else "k_fwd_wave"
     dk = kern[dom]
     achieved = dk["achieved_GBps"] or 0.0
 

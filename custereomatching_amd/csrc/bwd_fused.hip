@@ -431,6 +431,309 @@ __global__ __launch_bounds__(64) void k_bwd_sweep(Geo g, BwdArgs a) {
     bwd_sweep_body<K>(g, a, j, sg, rg, cbuf, pbuf);
 }
 
+// ---------------------------------------------------------------------------------------
+// Cooperative column sweep (default).  Same decomposition, partial layout and arithmetic
+// as k_bwd_sweep, but one WORKGROUP of 4 waves owns a (chunk, segment, row group) unit:
+// wave v owns rows y0 + 4v .. y0 + 4v + 3.  Per step every gradient element of the unit's
+// 16 + 2r rows is loaded and turned into A = g / S exactly once (own rows by their owner,
+// the 2r halo rows spread over the waves) and published in a double-buffered LDS row
+// array; after one barrier each wave forms the vertical k-row sums V of its own rows and
+// slides them horizontally with a k-deep LDS ring of its own V (HV += V(w) - V(w-k)).  So
+// the leaving column is never re-read (k_bwd_sweep re-reads it: ~1/3 of its HBM traffic)
+// and no halo row is loaded twice (the halo rows miss L2 in k_bwd_sweep), and the leaving
+// column's Y is not needed at all.
+constexpr int NWC = 4;          // waves per cooperative workgroup
+constexpr int TRW = TRB / NWC;  // own rows per wave
+
+// Finish 3 registers (each already summed over the 4 lanes {l, l+16, l+32, l+48}, one
+// value per 16-lane row): afterwards every lane holds the full 64-lane sum of one of the 12.
+__device__ __forceinline__ float reduce_tail3(float w0, float w1, float w2, int lane) {
+    const float x0 = pair_level<kMirror16, 8>(w0, w1, lane);
+    const float x1 = w2 + dpp<kMirror16>(w2);
+    const float y0 = pair_level<kMirror8, 4>(x0, x1, lane);
+    const float z = y0 + dpp<kQuad3210>(y0);
+    return z + dpp<kQuad1032>(z);
+}
+
+template <int K>
+__device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, int j, int sg, int rg, float* Abuf,
+                                              float* ring, float (*cbuf)[12], float (*pbuf)[12]) {
+    constexpr int R = K / 2, NY = TRB + 2 * R, NH = 2 * R;  // NH halo rows
+    constexpr int HPW = (NH + NWC - 1) / NWC;                // halo rows per wave (at most)
+    static_assert(NY <= 32, "two row-replicated registers cover the rows");
+
+    const ChunkGeo cg = chunk_geo(g, a.dlo, j);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int Wi = (int)g.W, Hi = (int)g.H;
+    const int d0 = (int)cg.d0, dl = d0 + lane;
+    const int64_t y0 = a.ylo + (int64_t)TRB * rg;
+    const int y0i = (int)y0;
+    int64_t xs64, xe64;
+    seg_cols(cg, R, sg, &xs64, &xe64);
+    const int xs = (int)xs64, xe = (int)xe64;
+    const int w0 = xs - R, wend = xe + R;
+    const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
+    int lwlo, lwhi;
+    if (window) {
+        lwlo = 0;
+        lwhi = (dl >= 0 && dl <= g.D) ? (int)g.WO : 0;
+    } else {
+        lwlo = dl < 0 ? -dl : 0;
+        lwhi = min((int)g.WO, Wi - dl);
+    }
+    const int gsU = (int)g.DO + (window ? 0 : 1);
+    const int slot = 2 * (j % a.Sj) + (sg & 1);
+    const size_t plane = (size_t)g.H * g.W;
+    const float cb = a.shift[0], pb = a.shift[1];
+
+    const uint32_t ib = (uint32_t)(plane * 4);
+    const auto rXc = make_rsrc(a.Xc, ib), rMc = make_rsrc(a.mcc, ib), rCc = make_rsrc(a.cc, ib);
+    const auto rYp = make_rsrc(a.Yp, ib), rMp = make_rsrc(a.mpp, ib), rPp = make_rsrc(a.pp, ib);
+    const size_t slab = (size_t)g.WO * g.DO;
+    const int64_t vrow0 = max(g.h_lo, y0 - R);
+    const auto rG = make_rsrc(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
+    const auto rV = make_rsrc(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
+    const int64_t ir0 = y0 - R;
+    const uint32_t vstride = (uint32_t)(slab * 4);
+    const int hlo = (int)g.h_lo, hhi = (int)g.h_hi, vrow0i = (int)vrow0;
+    auto img_off = [&](int row, int col) -> uint32_t {
+        return (row >= 0 && row < Hi && col >= 0 && col < Wi) ? (uint32_t)((row * Wi + col) * 4) : kOOB;
+    };
+    auto col_off = [&](int col) -> uint32_t { return (col >= 0 && col < Wi) ? (uint32_t)(col * 4) : kOOB; };
+
+    float HV[TRW];  // horizontal running sums of the vertical box sums V (own rows)
+    float P[3][TRW];
+#pragma unroll
+    for (int m = 0; m < TRW; ++m) {
+        HV[m] = 0.f;
+        P[0][m] = P[1][m] = P[2][m] = 0.f;
+    }
+    // ring[s][m][lane]: V of own row m at the step s (mod K) before
+#pragma unroll
+    for (int s = 0; s < K; ++s)
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) ring[(s * TRW + m) * 64 + lane] = 0.f;
+
+    const int yw = TRW * wv;  // first own row of this wave (unit row index)
+    const uint32_t prow_bytes = (uint32_t)(max((int64_t)0, min((int64_t)TRW, a.yhi - y0 - yw)) * g.W * 4);
+    auto part_rsrc = [&](int t) {
+        return make_rsrc(a.part + ((size_t)t * a.S + slot) * plane + (size_t)(y0 + yw) * g.W, prow_bytes);
+    };
+    auto flush = [&](int wfirst, int nsteps) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int jcol = ln & 15, m = ln >> 4;  // m: own row
+        const bool live = jcol < nsteps;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int p = 4 * t + m;
+            const int col = wfirst + jcol - (t == 0 ? R : 0);
+            const bool cok = live && col >= xs && col < xe && col >= 0 && col < Wi;
+            st_buf(cbuf[jcol][p], part_rsrc(t), cok ? (uint32_t)((m * Wi + col) * 4) : kOOB);
+            const int pcol = wfirst + jcol - 1 + (t == 0 ? -R : 0) + d0;
+            const uint32_t poff = (live && pcol >= 0 && pcol < Wi) ? (uint32_t)((m * Wi + pcol) * 4) : kOOB;
+            st_buf(pbuf[jcol][p], part_rsrc(3 + t), poff);
+        }
+    };
+    // which of the 12 camera sums (type * 4 + own row) each lane ends up with
+    int qlane;
+    {
+        const bool l0 = lane == 0;
+        auto mk = [&](int q) { return l0 ? (float)q : 0.f; };
+        const float w0r = red16(red32(mk(4), mk(8)), red32(mk(5), mk(9)));
+        const float w1r = red16(red32(mk(6), mk(10)), red32(mk(7), mk(11)));
+        const float w2r = red16(red32(mk(0), mk(1)), red32(mk(2), mk(3)));
+        qlane = (int)reduce_tail3(w0r, w1r, w2r, lane);
+    }
+
+    // rows of the unit this wave turns into A: its own rows, then its share of the halo
+    auto halo_row = [&](int q) { return q < R ? q : q + TRB; };  // q in [0, 2R)
+    constexpr int HP = HPW > 0 ? HPW : 1;
+
+    // ---- loads: issued one step ahead as inline asm (hand-counted waits; the compiler's
+    // own tracking would drain them at the loop header).  Rows by wave-uniform soffset
+    // (image rows clamped into the image: a clamped row only meets a zero gradient or feeds
+    // outputs that are not stored; volume rows outside the volume get an soffset past the
+    // descriptor, and the gfx950 range check includes soffset), columns by voffset. ----
+    auto iso = [&](int y) -> uint32_t {
+        int rr = (int)ir0 + y;
+        rr = rr < 0 ? 0 : rr >= Hi ? Hi - 1 : rr;
+        return (uint32_t)rr * (uint32_t)(Wi * 4);
+    };
+    auto vso = [&](int y) -> uint32_t {
+        const int row = (int)ir0 + y;
+        return (row >= hlo && row < hhi) ? (uint32_t)(row - vrow0i) * vstride : 0x7FFFFFF0u;
+    };
+    uint32_t sIo[TRW], sVo[TRW], sIh[HP], sVh[HP];
+#pragma unroll
+    for (int m = 0; m < TRW; ++m) {
+        sIo[m] = __builtin_amdgcn_readfirstlane(iso(R + yw + m));
+        sVo[m] = __builtin_amdgcn_readfirstlane(vso(R + yw + m));
+    }
+#pragma unroll
+    for (int i = 0; i < HP; ++i) {
+        const int q = wv + NWC * i;
+        const int y = halo_row(q < NH ? q : 0);
+        sIh[i] = __builtin_amdgcn_readfirstlane(iso(y));
+        sVh[i] = __builtin_amdgcn_readfirstlane(vso(y));
+    }
+    const i32x4 dG = make_rsrc_sgpr(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
+    const i32x4 dV = make_rsrc_sgpr(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
+    const i32x4 dY = make_rsrc_sgpr(a.Yp, ib), dM = make_rsrc_sgpr(a.mpp, ib), dP = make_rsrc_sgpr(a.pp, ib);
+    const i32x4 dX = make_rsrc_sgpr(a.Xc, ib), dMc = make_rsrc_sgpr(a.mcc, ib), dCc = make_rsrc_sgpr(a.cc, ib);
+    struct Ld {
+        uint32_t ge[TRW], cv[TRW], Ye[TRW], mp[TRW], pq[TRW], hg[HP], hY[HP], x0, x1, mc, cx;
+    };
+    auto issue = [&](int w, Ld& b) {
+        const int xb = w - R;
+        const bool ve = w >= lwlo && w < lwhi;
+        const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
+        const uint32_t oYe = col_off(w + dl), oPq = col_off(xb + dl);
+#pragma unroll
+        for (int m = 0; m < TRW; ++m)
+            asm_ld5s(b.ge[m], b.cv[m], b.Ye[m], b.mp[m], b.pq[m], oGe, oYe, oPq, dG, dV, dY, dM, dP, sVo[m], sIo[m]);
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+            const bool ok = wv + NWC * i < NH;
+            asm_ld2s(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dY, sVh[i], sIh[i]);
+        }
+        const int r16 = lane & 15;
+        asm_ld4(b.x0, b.x1, b.mc, b.cx, r16 < NY ? img_off((int)ir0 + r16, w) : kOOB,
+                16 + r16 < NY ? img_off((int)ir0 + 16 + r16, w) : kOOB, img_off(y0i + yw + (lane & 3), w),
+                img_off(y0i + yw + (lane & 3), xb), dX, dMc, dCc);
+    };
+    auto tie = [&](Ld& b) {
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) {
+            asm_tie(b.ge[m]); asm_tie(b.cv[m]); asm_tie(b.Ye[m]); asm_tie(b.mp[m]); asm_tie(b.pq[m]);
+        }
+#pragma unroll
+        for (int i = 0; i < HP; ++i) { asm_tie(b.hg[i]); asm_tie(b.hY[i]); }
+        asm_tie(b.x0); asm_tie(b.x1); asm_tie(b.mc); asm_tie(b.cx);
+    };
+    auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
+
+    int sidx = 0;  // ring slot of the current step (step count mod K)
+    auto step = [&](Ld& cur, Ld& nxt, int w, int s) {
+        // the only vector-memory operations since cur was issued: a flush's stores
+        asm_vmcnt<0>();
+        tie(cur);
+        issue(w + 1, nxt);  // past the segment's end: harmless, drained before the wave ends
+        float* Acur = Abuf + ((w - w0) & 1) * (NY * 64);
+        if (lane == 0) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                *(float4*)&pbuf[s][4 * t] = make_float4(P[t][0], P[t][1], P[t][2], P[t][3]);
+        }
+        const int xb = w - R;
+        const float tf = xb >= xs ? 1.f : 0.f, af = (w >= xs && w < xe) ? 1.f : 0.f;
+        const float mco = F(cur.mc) * af;
+        const float cxo = (F(cur.cx) - cb) * tf;
+        // X of unit row y (wave-uniform y): the lane of the row-replicated register that holds it
+        auto xrow = [&](int y) -> float {
+            const float x0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)cur.x0, y & 15));
+            const float x1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)cur.x1, y & 15));
+            return y >= 16 ? x1 : x0;
+        };
+        // ---- own rows: A, and the per-voxel terms (unit rows R + yw .. R + yw + 3) ----
+        float amv[TRW], bv[TRW];
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) {
+            const int y = R + yw + m;
+            const float Xf = xrow(y), Ye = F(cur.Ye[m]);
+            const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, Ye, kEps));
+            const float Ae = F(cur.ge[m]) * rSe;
+            Acur[y * 64 + lane] = Ae;
+            const float V = Ae * F(cur.cv[m]) * rSe;
+            amv[m] = Ae * F(cur.mp[m]);
+            bv[m] = V * Ye;
+            const float mcm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mco), m));
+            P[1][m] = shl1_add(P[1][m], Ae * mcm);
+            P[2][m] = shl1_add(P[2][m], (V * af) * Xf);
+        }
+#pragma unroll
+        for (int i = 0; i < HPW; ++i) {
+            const int q = wv + NWC * i;
+            if (q < NH) {
+                const int y = halo_row(q);
+                const float Xf = xrow(y);
+                Acur[y * 64 + lane] = F(cur.hg[i]) * __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, F(cur.hY[i]), kEps));
+            }
+        }
+        __syncthreads();  // the unit's A rows of this step are published
+        // ---- vertical k-row sums of own rows, horizontal slide through the ring ----
+        float col[TRW + 2 * R];
+#pragma unroll
+        for (int y = 0; y < TRW + 2 * R; ++y) col[y] = Acur[(yw + y) * 64 + lane];
+        float v = 0.f;
+#pragma unroll
+        for (int y = 0; y <= 2 * R; ++y) v += col[y];
+        float t1v[TRW];
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) {
+            if (m > 0) v = (v + col[m + 2 * R]) - col[m - 1];
+            float* rs = ring + (sidx * TRW + m) * 64 + lane;  // V of row m, K steps ago
+            HV[m] += v - *rs;
+            *rs = v;
+            t1v[m] = (F(cur.pq[m]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
+            const float cxm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxo), m));
+            P[0][m] = shl1_add(P[0][m], cxm * HV[m]);
+        }
+        sidx = sidx + 1 == K ? 0 : sidx + 1;
+        const float w0r = red16(red32(amv[0], bv[0]), red32(amv[1], bv[1]));
+        const float w1r = red16(red32(amv[2], bv[2]), red32(amv[3], bv[3]));
+        const float w2r = red16(red32(t1v[0], t1v[1]), red32(t1v[2], t1v[3]));
+        cbuf[s][qlane] = reduce_tail3(w0r, w1r, w2r, lane);
+    };
+
+    Ld L[2];
+    issue(w0, L[0]);
+    for (int wfirst = w0; wfirst < wend; wfirst += FB) {
+        const int nsteps = min(FB, wend - wfirst);  // FB is even: every block starts on L[0]
+        for (int s = 0; s < nsteps; s += 2) {
+            step(L[0], L[1], wfirst + s, s);
+            if (s + 1 >= nsteps) break;
+            step(L[1], L[0], wfirst + s + 1, s + 1);
+        }
+        flush(wfirst, nsteps);
+    }
+    // The last step's prefetch is still in flight: keep its registers live (the compiler would
+    // otherwise reuse them in the last flush) until it has landed.
+    asm_vmcnt<0>();
+    tie(L[0]);
+    tie(L[1]);
+    // ---- final projector state: lane l holds column (wend - 1) + off + d0 + l
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int col = wend - 1 + (t == 0 ? -R : 0) + d0 + lane;
+        const uint32_t c4 = (col >= 0 && col < g.W) ? (uint32_t)(col * 4) : kOOB;
+        const auto rp = part_rsrc(3 + t);
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) st_buf(P[t][m], rp, c4 == kOOB ? kOOB : c4 + (uint32_t)(m * Wi * 4));
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
+    // same unit order as k_bwd_sweep (one workgroup per unit)
+    const int64_t hb = blockIdx.x, xi = hb / 8, x = hb % 8;
+    const int nRGx = (a.nRG + 7) / 8;
+    const int64_t unit = xi / nRGx;
+    const int rg = (int)(x * nRGx + xi % nRGx);
+    if (rg >= a.nRG || unit >= (int64_t)a.nChunk * a.nsegMax) return;
+    const int j = chunk_of_rank((int)(unit / a.nsegMax), a.nChunk, a.jc);
+    const int sg = (int)(unit % a.nsegMax);
+    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
+    constexpr int NY = TRB + 2 * (K / 2);
+    __shared__ __attribute__((aligned(16))) float Abuf[2 * NY * 64];
+    __shared__ __attribute__((aligned(16))) float ring[NWC * K * TRW * 64];
+    __shared__ __attribute__((aligned(16))) float cbuf[NWC][FB][12];
+    __shared__ __attribute__((aligned(16))) float pbuf[NWC][FB][12];
+    const int wv = threadIdx.x >> 6;
+    bwd_coop_body<K>(g, a, j, sg, rg, Abuf, ring + wv * (K * TRW * 64), cbuf[wv], pbuf[wv]);
+}
+
 // Per (range class, column): the partial slots that hold the column (class 0 = camera
 // T1c / Am / B, which share one range; 1 = projector T1p; 2 = projector Ac / Bp).
 // cover layout: [3][W] counts, then [3][W][S] slot indices (uint16).
@@ -695,10 +998,16 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     const int64_t units = (int64_t)p.nChunk * p.nsegMax * p.nRG;
     const unsigned blocks = (unsigned)(8 * (int64_t)p.nChunk * p.nsegMax * cdiv(p.nRG, 8));
     if (units > 0) {
+        // CUSTMA_BWD_OLD=1: the one-wave-per-unit sweep (re-reads the leaving column), for comparison
+        const char* eo = getenv("CUSTMA_BWD_OLD");
+        const bool old = eo && atoi(eo) != 0;
         prof_begin(PROF_BWD, s);
         switch (g.k) {
-#define CUSTMA_K(KK) \
-    case KK: hipLaunchKernelGGL((k_bwd_sweep<KK>), dim3(blocks), dim3(64), 0, s, g, a); break;
+#define CUSTMA_K(KK)                                                                              \
+    case KK:                                                                                      \
+        if (old) hipLaunchKernelGGL((k_bwd_sweep<KK>), dim3(blocks), dim3(64), 0, s, g, a);        \
+        else hipLaunchKernelGGL((k_bwd_coop<KK>), dim3(blocks), dim3(64 * NWC), 0, s, g, a);      \
+        break;
             CUSTMA_SWEEP_KS(CUSTMA_K)
 #undef CUSTMA_K
             default: return hipErrorInvalidValue;

@@ -128,6 +128,44 @@ template <>
 __device__ __forceinline__ void asm_ld_raw<__half>(uint32_t& d, uint32_t off, i32x4 r) {
     asm volatile("buffer_load_ushort %0, %1, %2, 0 offen" : "=v"(d) : "v"(off), "s"(r));
 }
+// Grouped forms for code with SGPR pressure: a VALU write of an SGPR (e.g. the v_readlane
+// that restores a spilled descriptor) needs 5 wait states before a VMEM reads that SGPR
+// (gfx9 "VALU writes SGPR -> VMEM reads that SGPR"), and the compiler's hazard recognizer
+// does not look inside inline asm -- so each group starts with `s_nop 4`.  Outputs are
+// early-clobber: no destination may alias an address operand of a later load in the group.
+__device__ __forceinline__ void asm_ld5s(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t& a4,
+                                         uint32_t oA, uint32_t oB, uint32_t oC, i32x4 r0, i32x4 r1, i32x4 r2,
+                                         i32x4 r3, i32x4 r4, uint32_t sA, uint32_t sB) {
+    asm volatile(
+        "s_nop 4\n\t"
+        "buffer_load_dword %0, %5, %8, %13 offen\n\t"
+        "buffer_load_dword %1, %5, %9, %13 offen\n\t"
+        "buffer_load_dword %2, %6, %10, %14 offen\n\t"
+        "buffer_load_dword %3, %6, %11, %14 offen\n\t"
+        "buffer_load_dword %4, %7, %12, %14 offen"
+        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3), "=&v"(a4)
+        : "v"(oA), "v"(oB), "v"(oC), "s"(r0), "s"(r1), "s"(r2), "s"(r3), "s"(r4), "s"(sA), "s"(sB));
+}
+__device__ __forceinline__ void asm_ld2s(uint32_t& a0, uint32_t& a1, uint32_t oA, uint32_t oB, i32x4 r0, i32x4 r1,
+                                         uint32_t sA, uint32_t sB) {
+    asm volatile(
+        "s_nop 4\n\t"
+        "buffer_load_dword %0, %2, %4, %6 offen\n\t"
+        "buffer_load_dword %1, %3, %5, %7 offen"
+        : "=&v"(a0), "=&v"(a1)
+        : "v"(oA), "v"(oB), "s"(r0), "s"(r1), "s"(sA), "s"(sB));
+}
+__device__ __forceinline__ void asm_ld4(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t oA,
+                                        uint32_t oB, uint32_t oC, uint32_t oD, i32x4 r0, i32x4 r1, i32x4 r2) {
+    asm volatile(
+        "s_nop 4\n\t"
+        "buffer_load_dword %0, %4, %8, 0 offen\n\t"
+        "buffer_load_dword %1, %5, %8, 0 offen\n\t"
+        "buffer_load_dword %2, %6, %9, 0 offen\n\t"
+        "buffer_load_dword %3, %7, %10, 0 offen"
+        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+        : "v"(oA), "v"(oB), "v"(oC), "v"(oD), "s"(r0), "s"(r1), "s"(r2));
+}
 __device__ __forceinline__ void asm_ld_f64(double& d, uint32_t off, i32x4 r) {
     asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(d) : "v"(off), "s"(r));
 }

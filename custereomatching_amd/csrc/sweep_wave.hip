@@ -283,9 +283,12 @@ WaveGrid wave_grid(const Geo& g) {
 
 hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                            float* out, hipStream_t s) {
-    // CUSTMA_FWD_LDS=1: the workgroup (loader wave + LDS-staged stores) form, for comparison
+    // Full layout: the workgroup form (loader wave + LDS-staged, sector-owned stores) is
+    // faster -- this kernel's direct stores split 64-byte sectors between chunks there (C2:
+    // 1.35 vs 1.47 ms, WRITE_SIZE +10 %).  CUSTMA_FWD_LDS=0/1 overrides (benchmarking only).
     const char* e = getenv("CUSTMA_FWD_LDS");
-    if (e && atoi(e) != 0) return launch_fwd_lds(cam, proj, dtype, g, sc, sp, out, s);
+    const bool lds = e ? atoi(e) != 0 : g.layout != CUSTMA_LAYOUT_WINDOW;
+    if (lds) return launch_fwd_lds(cam, proj, dtype, g, sc, sp, out, s);
     if (dtype == CUSTMA_F16) return dispatch((const __half*)cam, (const __half*)proj, g, sc, sp, out, s);
     return dispatch((const float*)cam, (const float*)proj, g, sc, sp, out, s);
 }

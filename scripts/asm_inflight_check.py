@@ -61,6 +61,46 @@ def main():
     for x in issues[:40]:
         print(x)
 
+    # second screen: VALU writes an SGPR, a VMEM reads it within 5 wait states (gfx9 hazard;
+    # the compiler does not pad inline asm for it)
+    def sregs(text):
+        out = set()
+        for a, b, c in re.findall(r"s\[(\d+):(\d+)\]|\bs(\d+)\b", text):
+            if c:
+                out.add(int(c))
+            else:
+                out |= set(range(int(a), int(b) + 1))
+        return out
+
+    recent = []  # (wait states since, sgprs written)
+    haz = []
+    for i in range(start + 1, len(lines)):
+        t = lines[i].strip()
+        if t.startswith(".Lfunc_end"):
+            break
+        if not t or t.startswith(";") or t.startswith("."):
+            continue
+        parts = t.split(None, 1)
+        op, args = parts[0], (parts[1] if len(parts) > 1 else "")
+        if op.startswith(("buffer_", "global_")):
+            used = sregs(args)
+            for ws, regs_w in recent:
+                if ws < 5 and used & regs_w:
+                    haz.append((i + 1, t, sorted(used & regs_w), ws))
+        n = 1
+        m = re.match(r"s_nop\s+(\d+)", t)
+        if m:
+            n = int(m.group(1)) + 1
+        recent = [(ws + n, r) for ws, r in recent if ws + n < 5]
+        if op.startswith("v_"):
+            dst = args.split(",")[0] if args else ""
+            w = sregs(dst)
+            if w:
+                recent.append((0, w))
+    print(f"{len(haz)} VMEM instructions read an SGPR written by VALU < 5 wait states earlier")
+    for x in haz[:20]:
+        print(x)
+
 
 if __name__ == "__main__":
     main()
