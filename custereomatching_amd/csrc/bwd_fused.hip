@@ -444,6 +444,7 @@ __global__ __launch_bounds__(64) void k_bwd_sweep(Geo g, BwdArgs a) {
 // column's Y is not needed at all.
 constexpr int NWC = 4;          // waves per cooperative workgroup
 constexpr int TRW = TRB / NWC;  // own rows per wave
+constexpr int FBC = 8;          // steps per flush (small buffers: 3 workgroups per CU at k = 9)
 
 // Finish 3 registers (each already summed over the 4 lanes {l, l+16, l+32, l+48}, one
 // value per 16-lane row): afterwards every lane holds the full 64-lane sum of one of the 12.
@@ -523,8 +524,9 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     auto flush = [&](int wfirst, int nsteps) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        const int jcol = ln & 15, m = ln >> 4;  // m: own row
-        const bool live = jcol < nsteps;
+        // lanes 0-31: step jcol, own row m (the upper half idles)
+        const int jcol = ln & (FBC - 1), m = (ln / FBC) & 3;
+        const bool live = jcol < nsteps && ln < 4 * FBC;
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             const int p = 4 * t + m;
@@ -689,8 +691,8 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 
     Ld L[2];
     issue(w0, L[0]);
-    for (int wfirst = w0; wfirst < wend; wfirst += FB) {
-        const int nsteps = min(FB, wend - wfirst);  // FB is even: every block starts on L[0]
+    for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
+        const int nsteps = min(FBC, wend - wfirst);  // FBC is even: every block starts on L[0]
         for (int s = 0; s < nsteps; s += 2) {
             step(L[0], L[1], wfirst + s, s);
             if (s + 1 >= nsteps) break;
@@ -728,8 +730,8 @@ __global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
     constexpr int NY = TRB + 2 * (K / 2);
     __shared__ __attribute__((aligned(16))) float Abuf[2 * NY * 64];
     __shared__ __attribute__((aligned(16))) float ring[NWC * K * TRW * 64];
-    __shared__ __attribute__((aligned(16))) float cbuf[NWC][FB][12];
-    __shared__ __attribute__((aligned(16))) float pbuf[NWC][FB][12];
+    __shared__ __attribute__((aligned(16))) float cbuf[NWC][FBC][12];
+    __shared__ __attribute__((aligned(16))) float pbuf[NWC][FBC][12];
     const int wv = threadIdx.x >> 6;
     bwd_coop_body<K>(g, a, j, sg, rg, Abuf, ring + wv * (K * TRW * 64), cbuf[wv], pbuf[wv]);
 }
