@@ -16,7 +16,7 @@ exchanges k//2 halo rows with its neighbours over RCCL (custereomatching_amd.
 rowband); no other collective on the data path.
 
 Prints ONE JSON line (rank 0).  Extra objects:
-  roofline      dominant kernel (the backward sweep, k_bwd_sweep) -- algorithmic
+  roofline      dominant kernel (the backward sweep, k_bwd_coop) -- algorithmic
                 bytes / its average duration from HIP events around its launches in
                 the timed region; "kernels" has the same for the forward sweep
   cpu_baseline  the reference's torch CPU path (oracle/torch_ref.py restating
@@ -246,13 +246,15 @@ def main():
     img = 2 * H * W * 4
     fwd_bytes = nvox_rank * 4 + img
     bwd_bytes = 2 * nvox_rank * 4 + img + img
+    # forward sweep kernel by layout (sweep_wave.hip launch_fwd_fast): full -> k_sweep_fwd, window -> k_fwd_wave
+    fwd_name = "k_sweep_fwd" if args.layout == "full" else "k_fwd_wave"
     kern = {
-        "k_fwd_wave": {"avg_launch_ms": round(fwd_kms, 4), "launches": n_fk, "algorithmic_bytes": fwd_bytes,
+        fwd_name: {"avg_launch_ms": round(fwd_kms, 4), "launches": n_fk, "algorithmic_bytes": fwd_bytes,
                         "achieved_GBps": round(fwd_bytes / (fwd_kms * 1e-3) / 1e9, 1) if fwd_kms else None},
-        "k_bwd_sweep": {"avg_launch_ms": round(bwd_kms, 4), "launches": n_bk, "algorithmic_bytes": bwd_bytes,
+        "k_bwd_coop": {"avg_launch_ms": round(bwd_kms, 4), "launches": n_bk, "algorithmic_bytes": bwd_bytes,
                         "achieved_GBps": round(bwd_bytes / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None},
     }
-    dom = "k_bwd_sweep" if bwd_kms >= fwd_kms else "k_fwd_wave"
+    dom = "k_bwd_coop" if bwd_kms >= fwd_kms else fwd_name
     dk = kern[dom]
     achieved = dk["achieved_GBps"] or 0.0
 

@@ -153,6 +153,7 @@ inline SweepGrid sweep_grid(const Geo& g, bool owned = false) {
 // 64 diagonals).
 struct WaveGrid {
     int nChunk, nTile, nBand, TH;
+    bool rem;  // window, (D+1) % 64 == 1: the last chunk's waves add diagonal D
 };
 WaveGrid wave_grid(const Geo& g);
 hipError_t launch_fwd_lds(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,

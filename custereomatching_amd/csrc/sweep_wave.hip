@@ -38,11 +38,14 @@ typedef __attribute__((address_space(3))) volatile float lds_vf;
 
 constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
 
-template <int K, typename T, bool FULL_EDGE>
+// REM: this wave (window layout, last chunk, (D+1) % 64 == 1) also computes the single
+// remainder diagonal d0 + 64 = D: lane x < 16 + 2r keeps its column sum, the horizontal box
+// is summed from LDS, and lanes m < 16 store volume column D of tile row m.
+template <int K, typename T, bool FULL_EDGE, bool REM>
 __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
                                           const Stats& sc, const Stats& sp, float* __restrict__ out,
                                           int64_t u0, int64_t h0, int64_t h1, int64_t d0,
-                                          double* rowE, double* rowL, double* sM, float* sQ) {
+                                          double* rowE, double* rowL, double* sM, float* sQ, double* sR) {
     constexpr int R = K / 2, NX = TW + 2 * R;
     static_assert(NX + 63 <= kRowP && NX <= 32, "row segment fits the LDS slice and two broadcast registers");
     constexpr uint32_t OOB = 0x80000000u;
@@ -57,10 +60,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         return (have && x >= 0 && x < g.W) ? (uint32_t)(x * esz) : OOB;
     };
     const int64_t xO0 = u0 - R + d0, oS = u0 + d0;
-    const uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 63, xO0 + 64 + l, sizeof(T));
+    const uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 64, xO0 + 64 + l, sizeof(T));
     const uint32_t vC0 = colOff(true, u0 - R + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R + 16 + r16, sizeof(T));
-    const uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 63, oS + 64 + l, 8);
-    const uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 63, oS + 64 + l, 4);
+    const uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 64, oS + 64 + l, 8);
+    const uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 64, oS + 64 + l, 4);
     const uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
     auto row_rsrc = [&](const void* base, int64_t row, int esz, bool ok) {
         ok = ok && row >= 0 && row < g.H;
@@ -116,6 +119,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     double col[NX];
 #pragma unroll
     for (int x = 0; x < NX; ++x) col[x] = 0.0;
+    double colR = 0.0;  // REM: column sum of diagonal d0 + 64 for column x = lane (lanes < NX)
 
     // The loads of step t are issued at the end of step t-2.  The first two issues happen in
     // two warm-up iterations of the loop itself (t = hs-2, hs-1: loads only), not in a
@@ -126,7 +130,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     auto compute = [&](Stage& p, int64_t t) {
         // loads(t) were issued at the end of step t-2; after them: the stores of step t-1
         // (16, from step h0 on) and the loads of step t+1
-        if (t - 1 >= h0) asm_vmcnt<kLoads + TW>();
+        if (t - 1 >= h0) asm_vmcnt<kLoads + TW + (REM ? 1 : 0)>();
         else asm_vmcnt<kLoads>();
         tie(p);
         rowE[l] = raw_to_f64<T>(p.pe0);
@@ -180,6 +184,11 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             });
         }
 
+        if constexpr (REM) {
+            const double cRe = l < 16 ? ca0 : ca1, cRl = l < 16 ? cb0 : cb1;  // camera column u0 - R + l
+            colR = __builtin_fma(cRe, *(const lds_vd*)(rowE + 64 + l), colR);
+            colR = __builtin_fma(cRl, *(const lds_vd*)(rowL + 64 + l), colR);
+        }
         if (t >= h0) {
             const auto rOut = make_rsrc(out + ((t - g.h_lo) * g.WO + u0) * DO, tile_bytes);
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
@@ -203,6 +212,20 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, so,
                                                       CUSTMA_STORE_AUX);
             });
+            if constexpr (REM) {
+                // diagonal D for tile row m = lane: box over the column sums of lanes m .. m + 2R
+                sR[l] = colR;
+                double sr = (double)kEps;
+                const lds_vd* rr = (const lds_vd*)(sR + (l & 15));
+#pragma unroll
+                for (int x = 0; x < 2 * R + 1; ++x) sr += rr[x];
+                const double e = __builtin_fma(nb, *(const lds_vd*)(sM + 64 + (l & 15)), sr);
+                const float den2 = __builtin_fmaf(uq, *(const lds_vf*)(sQ + 64 + (l & 15)), kEps);
+                const float c = (float)e * __builtin_amdgcn_rsqf(den2);
+                const uint32_t vo = l < 16 ? (uint32_t)((l * DO + g.D) * 4) : OOB;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, 0u,
+                                                      CUSTMA_STORE_AUX);
+            }
         }
     };
     auto step = [&](auto kc, int64_t t) {
@@ -226,6 +249,7 @@ __global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, cons
                                                  Stats sc, Stats sp, float* __restrict__ out, WaveGrid wg) {
     __shared__ __attribute__((aligned(16))) double rowE[kRowP], rowL[kRowP], sM[kRowP];
     __shared__ __attribute__((aligned(16))) float sQ[kRowP];
+    __shared__ __attribute__((aligned(16))) double sR[64];
     const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
     const int chunk = (int)(bid % wg.nChunk);
     const int64_t rest = bid / wg.nChunk;
@@ -239,9 +263,11 @@ __global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, cons
     // full layout: a chunk with a voxel outside [0, W) for some tile row needs per-row masks
     const bool edge = !window && (u0 + d0 < 0 || u0 + TW - 1 + d0 + 63 >= g.W);
     if (edge)
-        wave_body<K, T, true>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ);
+        wave_body<K, T, true, false>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ, sR);
+    else if (window && wg.rem && chunk == wg.nChunk - 1)
+        wave_body<K, T, false, true>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ, sR);
     else
-        wave_body<K, T, false>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ);
+        wave_body<K, T, false, false>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ, sR);
 }
 
 template <int K, typename T>
@@ -271,6 +297,10 @@ WaveGrid wave_grid(const Geo& g) {
     WaveGrid wg;
     const int64_t nd = g.layout == CUSTMA_LAYOUT_WINDOW ? (int64_t)g.D + 1 : g.W + TW - 1;
     wg.nChunk = (int)cdiv(nd, 64);
+    // window with (D+1) % 64 == 1 (D = 64 n): the last full chunk's waves also compute the
+    // single remainder diagonal D (no fifth, nearly idle chunk of waves)
+    wg.rem = g.layout == CUSTMA_LAYOUT_WINDOW && nd > 64 && nd % 64 == 1 && !getenv("CUSTMA_WAVE_NOREM");
+    if (wg.rem) --wg.nChunk;
     wg.nTile = (int)cdiv(g.WO, TW);
     // tuning override (benchmarking only): CUSTMA_WAVE_TH
     const char* e = getenv("CUSTMA_WAVE_TH");

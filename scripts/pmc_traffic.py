@@ -46,7 +46,7 @@ print(f"calibration: FETCH bytes/unit dword={f_rd1:.1f} x4={f_rd4:.1f}; WRITE by
 bench = ["python3", "bench.py", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-north-star",
          "--layout", layout]
 meas = {c: run(c, "bench", bench) for c in ("FETCH_SIZE", "WRITE_SIZE")}
-for kern in ("k_bwd_sweep", "k_fwd_wave"):
+for kern in ("k_bwd_coop", "k_sweep_fwd", "k_fwd_wave"):
     fs, ws = mean_of(meas["FETCH_SIZE"], kern), mean_of(meas["WRITE_SIZE"], kern)
     if fs is None or ws is None:
         continue

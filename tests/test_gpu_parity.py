@@ -80,6 +80,41 @@ def test_fast_forward_within_bound(gpu, case, layout):
     assert np.abs(got - truth).max() <= O.cost_error_bound(k)
 
 
+REM_CASES = [
+    # window D = 64 n: D + 1 diagonals, the last one computed by the final chunk's waves
+    (24, 100, 5, 64, torch.float32),
+    (20, 200, 9, 128, torch.float32),
+    (18, 300, 11, 256, torch.float16),
+    (19, 90, 15, 64, torch.float32),
+]
+
+
+@pytest.mark.parametrize("case", REM_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_D{c[3]}" for c in REM_CASES])
+def test_fast_forward_window_remainder_diagonal(gpu, case):
+    H, W, k, D, dt = case
+    cam, proj = make_pair(H, W, D, seed=21)
+    if dt == torch.float16:
+        cam = cam.astype(np.float16).astype(np.float32)
+        proj = proj.astype(np.float16).astype(np.float32)
+    ref = O.forward(cam, proj, k, layout=O.WINDOW, D=D, contract=1)
+    got = gpu_forward(cam, proj, k, WIN, D, "fast", gpu, dtype=dt)
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() <= O.cost_error_bound(k)
+
+
+@pytest.mark.parametrize("lds_form", ["0", "1"])
+@pytest.mark.parametrize("layout", [FULL, WIN])
+def test_fast_forward_both_kernel_forms(gpu, monkeypatch, lds_form, layout):
+    # CUSTMA_FWD_LDS selects the forward kernel form (LDS-loader or wave-independent sweep)
+    monkeypatch.setenv("CUSTMA_FWD_LDS", lds_form)
+    H, W, k, D = 40, 150, 9, 64
+    cam, proj = make_pair(H, W, D, seed=22)
+    lay, Dl = _layout_args(layout, D)
+    ref = O.forward(cam, proj, k, layout=lay, D=Dl, contract=1)
+    got = gpu_forward(cam, proj, k, layout, D, "fast", gpu)
+    assert np.abs(got - ref).max() <= O.cost_error_bound(k)
+
+
 @pytest.mark.parametrize("precision", ["exact", "fast"])
 def test_fp16_inputs(gpu, precision):
     H, W, k, D = 32, 64, 9, 20
