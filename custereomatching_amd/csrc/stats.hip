@@ -11,17 +11,22 @@
 //   then k column taps), 2k fp64 adds per pixel instead of k^2.
 // sqt: fp64-accurate centred second moment box2 - box^2 / k^2 (separable too), rounded
 //   to fp32; only the backward reads it.
+#include <type_traits>
+
 #include "common.h"
+#include "sweep.h"
 
 namespace custma {
 
 namespace {
 constexpr int TX = 16, TY = 64, PR = 4;  // 16 x 64 pixels per 256-thread workgroup, 4 rows per thread
 
-template <typename T>
+// KT > 0: the window size as a compile-time constant (the sweep's instantiations), so the
+// k^2 tap loops unroll and the per-pixel row masks fold away; KT = 0: runtime k.
+template <typename T, int KT>
 __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g, Stats st) {
     extern __shared__ __attribute__((aligned(16))) double lds_d[];
-    const int k = g.k, r = g.r, LX = TX + 2 * r, LY = TY + 2 * r;
+    const int k = KT > 0 ? KT : g.k, r = k / 2, LX = TX + 2 * r, LY = TY + 2 * r;
     double* rs = lds_d;                    // [LY][TX] fp64 k-tap row sums
     double* rs2 = rs + LY * TX;            // [LY][TX] fp64 k-tap row sums of squares
     float* tile = (float*)(rs2 + LY * TX);  // [LY][LX] zero-padded image tile
@@ -35,6 +40,7 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g,
         const int ty = e / TX, tx = e % TX;
         const float* t = tile + ty * LX + tx;
         double a = 0.0, b = 0.0;
+#pragma unroll
         for (int j = 0; j < k; ++j) {
             const double v = (double)t[j];
             a += v;
@@ -51,7 +57,9 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g,
     float m[PR], sq[PR];
 #pragma unroll
     for (int p = 0; p < PR; ++p) { m[p] = 0.f; sq[p] = 0.f; }
+#pragma unroll
     for (int i2 = 0; i2 < k + PR - 1; ++i2)
+#pragma unroll
         for (int j = 0; j < k; ++j) {
             const float v = t[i2 * LX + j];
 #pragma unroll
@@ -60,7 +68,9 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g,
         }
 #pragma unroll
     for (int p = 0; p < PR; ++p) m[p] = m[p] / (float)(k * k);
+#pragma unroll
     for (int i2 = 0; i2 < k + PR - 1; ++i2)
+#pragma unroll
         for (int j = 0; j < k; ++j) {
             const float v = t[i2 * LX + j];
 #pragma unroll
@@ -78,6 +88,7 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g,
         const int64_t y = y0 + ly;
         if (y >= g.H) break;
         double b = 0.0, b2 = 0.0;
+#pragma unroll
         for (int i = 0; i < k; ++i) {
             b += rs[(ly + i) * TX + lx];
             b2 += rs2[(ly + i) * TX + lx];
@@ -96,10 +107,20 @@ hipError_t launch_stats(const void* img, int dtype, const Geo& g, Stats st, hipS
     const dim3 grid((unsigned)cdiv(g.W, TX), (unsigned)cdiv(g.H, TY));
     const int LX = TX + 2 * g.r, LY = TY + 2 * g.r;
     const size_t lds = sizeof(double) * 2 * LY * TX + sizeof(float) * LY * LX;
-    if (dtype == CUSTMA_F16)
-        hipLaunchKernelGGL(k_stats<__half>, grid, dim3(256), lds, s, (const __half*)img, g, st);
-    else
-        hipLaunchKernelGGL(k_stats<float>, grid, dim3(256), lds, s, (const float*)img, g, st);
+    auto go = [&](auto kc) {
+        constexpr int KT = decltype(kc)::value;
+        if (dtype == CUSTMA_F16)
+            hipLaunchKernelGGL((k_stats<__half, KT>), grid, dim3(256), lds, s, (const __half*)img, g, st);
+        else
+            hipLaunchKernelGGL((k_stats<float, KT>), grid, dim3(256), lds, s, (const float*)img, g, st);
+    };
+    switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: go(std::integral_constant<int, KK>{}); break;
+        CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+        default: go(std::integral_constant<int, 0>{});
+    }
     return hipGetLastError();
 }
 

@@ -41,15 +41,25 @@ constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
 // REM: this wave (window layout, last chunk, (D+1) % 64 == 1) also computes the single
 // remainder diagonal d0 + 64 = D: lane x < 16 + 2r keeps its column sum, the horizontal box
 // is summed from LDS, and lanes m < 16 store volume column D of tile row m.
-template <int K, typename T, bool FULL_EDGE, bool REM>
+//
+// STAGED (window layout, k_fwd_tile): the workgroup holds every diagonal chunk of one
+// column tile; each wave puts its 16 x 64 outputs of a step into an LDS image of the 16
+// contiguous volume rows (two step buffers), and after one barrier the workgroup stores
+// the whole 16 * DO-float block with dword stores, SS per thread (OOB-masked, so every
+// thread issues exactly SS and the hand-counted vmcnt holds): every volume sector is
+// written once, by one workgroup, in one burst.
+template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2>
 __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
                                           const Stats& sc, const Stats& sp, float* __restrict__ out,
                                           int64_t u0, int64_t h0, int64_t h1, int64_t d0,
-                                          double* rowE, double* rowL, double* sM, float* sQ, double* sR) {
+                                          double* rowE, double* rowL, double* sM, float* sQ, double* sR,
+                                          float* stage = nullptr) {
     constexpr int R = K / 2, NX = TW + 2 * R;
     static_assert(NX + 63 <= kRowP && NX <= 32, "row segment fits the LDS slice and two broadcast registers");
     constexpr uint32_t OOB = 0x80000000u;
-    const int l = threadIdx.x, r16 = l & 15;
+    // SS (STAGED): dword stores per thread per step, the same for every wave of the workgroup;
+    // SS < 0: -SS 16-byte stores + one dword store (the block's < 4-float tail) per thread
+    const int l = threadIdx.x & 63, r16 = l & 15;
     const int64_t hs = h0 - 2 * R;  // 2R warm-up steps fill the column sums
     const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
     const double rk2 = 1.0 / (double)(K * K);
@@ -90,8 +100,13 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         asm_ld_raw<T>(p.cl0, vC0, rCl);
         asm_ld_raw<T>(p.cl1, vC1, rCl);
         const bool st = t >= h0 && t < h1;
-        const auto rPB = row_rsrc(sp.box, t, 8, st), rPS = row_rsrc(sp.sq, t, 4, st);
-        const auto rCB = row_rsrc(sc.box, t, 8, st), rCS = row_rsrc(sc.sq, t, 4, st);
+#ifdef CUSTMA_ABL_STATS7  // ablation builds only: statistics always from row 7 (L2-resident)
+        const int64_t ts = 7;
+#else
+        const int64_t ts = t;
+#endif
+        const auto rPB = row_rsrc(sp.box, ts, 8, st), rPS = row_rsrc(sp.sq, ts, 4, st);
+        const auto rCB = row_rsrc(sc.box, ts, 8, st), rCS = row_rsrc(sc.sq, ts, 4, st);
         asm_ld_f64(p.m0, vM0, rPB);
         asm_ld_f64(p.m1, vM1, rPB);
         asm_ld_raw<float>(p.q0, vQ0, rPS);
@@ -119,19 +134,33 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     double col[NX];
 #pragma unroll
     for (int x = 0; x < NX; ++x) col[x] = 0.0;
+    float sink = 0.f;   // CUSTMA_ABL_NOSTORE: keeps the outputs live
     double colR = 0.0;  // REM: column sum of diagonal d0 + 64 for column x = lane (lanes < NX)
 
-    // The loads of step t are issued at the end of step t-2.  The first two issues happen in
-    // two warm-up iterations of the loop itself (t = hs-2, hs-1: loads only), not in a
+    // The loads of step t are issued at the end of step t-P (P = 2, or 3 in the staged
+    // kernel).  The first P issues happen in P warm-up iterations of the loop itself
+    // (t = hs-P .. hs-1: loads only), not in a
     // prologue: the compiler believes an asm load's destination is written when the asm
     // issues, so a peeled prologue with another register assignment would be joined to the
     // loop by register copies -- reads of registers whose loads are still in flight.
-    Stage st[2];
+    Stage st[P];
     auto compute = [&](Stage& p, int64_t t) {
-        // loads(t) were issued at the end of step t-2; after them: the stores of step t-1
-        // (16, from step h0 on) and the loads of step t+1
-        if (t - 1 >= h0) asm_vmcnt<kLoads + TW + (REM ? 1 : 0)>();
-        else asm_vmcnt<kLoads>();
+        // loads(t) were issued at the end of step t-P; after them, for each step s in
+        // t-P+1 .. t-1: its stores (from step h0 on) and loads(s+P)
+        constexpr int ST = STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);  // stores per step
+        static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
+#ifdef CUSTMA_ABL_NOWAIT  // ablation builds only: no wait for the loads (garbage values)
+        asm_vmcnt<63>();
+#else
+        if constexpr (P == 3) {
+            if (t - 2 >= h0) asm_vmcnt<2 * (kLoads + ST)>();
+            else if (t - 1 >= h0) asm_vmcnt<2 * kLoads + ST>();
+            else asm_vmcnt<2 * kLoads>();
+        } else {
+            if (t - 1 >= h0) asm_vmcnt<kLoads + ST>();
+            else asm_vmcnt<kLoads>();
+        }
+#endif
         tie(p);
         rowE[l] = raw_to_f64<T>(p.pe0);
         rowE[64 + l] = raw_to_f64<T>(p.pe1);
@@ -147,6 +176,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         const float uq = __builtin_bit_cast(float, p.uq);  // camera ex2 of column r16
 
         // ---- col[x] += c(enter, x) p(enter, x + delta) - c(leave, x) p(leave, x + delta) ----
+#ifndef CUSTMA_ABL_NOUPDATE  // ablation builds only (scripts/build_ablations.py)
         {
             const lds_vd* oa = (const lds_vd*)(rowE + l);
             const lds_vd* ob = (const lds_vd*)(rowL + l);
@@ -183,6 +213,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 }
             });
         }
+#endif
 
         if constexpr (REM) {
             const double cRe = l < 16 ? ca0 : ca1, cRl = l < 16 ? cb0 : cb1;  // camera column u0 - R + l
@@ -196,6 +227,8 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
             const lds_vd* mrow = (const lds_vd*)(sM + l);
             const lds_vf* qrow = (const lds_vf*)(sQ + l);
+            lds_vf* sb = (lds_vf*)(stage + (t & 1) * TW * DO);  // STAGED: this step's buffer
+            const bool dv = d0 + l <= g.D;
             Unroll<0, TW>::run([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
                 if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
@@ -203,14 +236,27 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 float den2 = kEps;
                 // E + eps = S + eps - box_c * mean_p;  ex2 * ey2 + eps
                 fin_bc<m>(e, den2, nb, mrow[m], uq, qrow[m]);
+#ifdef CUSTMA_ABL_NOOUT
+                const float c = (float)m;
+#else
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
+#endif
                 uint32_t vo = vOut, so = (uint32_t)(m * sstep);
                 if constexpr (FULL_EDGE) {  // per-row mask; the whole offset in voffset
                     vo = ((uint64_t)(a0 + m) < (uint64_t)g.W) ? (uint32_t)((a0 + m + m * DO) * 4) : OOB;
                     so = 0;
                 }
+#ifdef CUSTMA_ABL_NOSTORE
+                sink += c;
+                (void)dv;
+                (void)sb;
+#else
+                if constexpr (STAGED) {
+                    if (dv) sb[m * DO + d0 + l] = c;
+                } else
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, so,
                                                       CUSTMA_STORE_AUX);
+#endif
             });
             if constexpr (REM) {
                 // diagonal D for tile row m = lane: box over the column sums of lanes m .. m + 2R
@@ -222,26 +268,71 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 const double e = __builtin_fma(nb, *(const lds_vd*)(sM + 64 + (l & 15)), sr);
                 const float den2 = __builtin_fmaf(uq, *(const lds_vf*)(sQ + 64 + (l & 15)), kEps);
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
-                const uint32_t vo = l < 16 ? (uint32_t)((l * DO + g.D) * 4) : OOB;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, 0u,
-                                                      CUSTMA_STORE_AUX);
+                if constexpr (STAGED) {
+                    if (l < 16) sb[l * DO + g.D] = c;
+                } else {
+                    const uint32_t vo = l < 16 ? (uint32_t)((l * DO + g.D) * 4) : OOB;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, 0u,
+                                                          CUSTMA_STORE_AUX);
+                }
             }
+#ifndef CUSTMA_ABL_NOSTORE
+            if constexpr (STAGED) {
+                // every wave's part of the 16 rows is in LDS: store the block (256 contiguous
+                // bytes per wave instruction, the whole workgroup's instruction contiguous)
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                const int NT = (int)blockDim.x, tid = (int)threadIdx.x;
+                const int total = (int)(nrow * DO);
+                if constexpr (SS < 0) {  // block base 16-byte aligned (checked at launch)
+                    const int n4 = total >> 2;
+                    typedef __attribute__((address_space(3))) volatile i32x4 lds_v4;
+#pragma unroll
+                    for (int i = 0; i < -SS; ++i) {
+                        const int j = i * NT + tid;
+                        const i32x4 v = ((lds_v4*)sb)[j < n4 ? j : 0];
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rOut, j < n4 ? (uint32_t)(j * 16) : OOB, 0u,
+                                                               CUSTMA_STORE_AUX);
+                    }
+                    const int j = 4 * n4 + tid;
+                    const float v = sb[j < total ? j : 0];
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), rOut,
+                                                          (tid < 4 && j < total) ? (uint32_t)(j * 4) : OOB, 0u,
+                                                          CUSTMA_STORE_AUX);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < SS; ++i) {
+                        const int idx = i * NT + tid;
+                        const float v = sb[idx < total ? idx : 0];
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), rOut,
+                                                              idx < total ? (uint32_t)(idx * 4) : OOB, 0u,
+                                                              CUSTMA_STORE_AUX);
+                    }
+                }
+            }
+#endif
         }
     };
     auto step = [&](auto kc, int64_t t) {
         Stage& p = st[decltype(kc)::value];
         if (t >= hs) compute(p, t);
-        load_step(t + 2, p);  // past the band's end: harmless (rows out of range read zeros)
+        load_step(t + P, p);  // past the band's end: harmless (rows out of range read zeros)
     };
-    int64_t t_first = hs - 2;  // opaque: the warm-up iterations must not be peeled
+    int64_t t_first = hs - P;  // opaque: the warm-up iterations must not be peeled
     asm volatile("" : "+s"(t_first));
-    for (int64_t t = t_first;; t += 2) {
+    for (int64_t t = t_first;; t += P) {
         step(std::integral_constant<int, 0>{}, t);
         if (t + 1 >= h1) break;
         step(std::integral_constant<int, 1>{}, t + 1);
         if (t + 2 >= h1) break;
+        if constexpr (P == 3) {
+            step(std::integral_constant<int, 2 % P>{}, t + 2);
+            if (t + 3 >= h1) break;
+        }
     }
     asm_vmcnt<0>();  // every wave drains its own loads before it ends
+#ifdef CUSTMA_ABL_NOSTORE
+    if (sink == 1.2345f) out[l] = sink;
+#endif
 }
 
 template <int K, typename T>
@@ -270,12 +361,76 @@ __global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, cons
         wave_body<K, T, false, false>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ, sR);
 }
 
+// Window layout, D + 1 <= 64 * kTileMaxChunks (+1): one workgroup per (column tile, row
+// band) holding all diagonal chunks, wave w = chunk w (the last one also takes the
+// remainder diagonal when wg.rem); outputs leave through the LDS block image (STAGED).
+constexpr int kTileMaxChunks = 4;
+#ifndef CUSTMA_TILE_P
+#define CUSTMA_TILE_P 2
+#endif
+constexpr int kTileP = CUSTMA_TILE_P;  // load pipeline depth (steps)
+constexpr int kWaveLds = (3 * kRowP + 64) * 8 + kRowP * 4;  // rowE, rowL, sM, sR (f64) + sQ (f32)
+
+template <int K, typename T, bool X4>
+#ifndef CUSTMA_TILE_WPE
+#define CUSTMA_TILE_WPE 1
+#endif
+__global__ __launch_bounds__(64 * kTileMaxChunks) __attribute__((amdgpu_waves_per_eu(CUSTMA_TILE_WPE))) void k_fwd_tile(const T* __restrict__ cam,
+                                                                 const T* __restrict__ proj, Geo g, Stats sc,
+                                                                 Stats sp, float* __restrict__ out, WaveGrid wg) {
+    extern __shared__ __attribute__((aligned(16))) double lds_t[];
+    const int w = (int)(threadIdx.x >> 6);
+    char* mine = (char*)lds_t + w * kWaveLds;
+    double* rowE = (double*)mine;
+    double* rowL = rowE + kRowP;
+    double* sM = rowL + kRowP;
+    double* sR = sM + kRowP;
+    float* sQ = (float*)(sR + 64);
+    float* stage = (float*)((char*)lds_t + wg.nChunk * kWaveLds);
+    const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int wt = (int)(bid % wg.nTile);
+    const int band = (int)(bid / wg.nTile);
+    const int64_t u0 = (int64_t)wt * TW;
+    const int64_t h0 = g.h_lo + (int64_t)band * wg.TH, h1 = min(g.h_hi, h0 + wg.TH);
+    const int64_t d0 = (int64_t)w * 64;
+    // SS stores per thread cover the 16 DO-float block: DO <= 64 nChunk, or 64 nChunk + 1 (rem);
+    // X4: 4 (5 with rem) 16-byte stores per thread
+    constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
+    if (!wg.rem)
+        wave_body<K, T, false, false, true, S0, kTileP>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ, sR,
+                                                stage);
+    else if (w == wg.nChunk - 1)
+        wave_body<K, T, false, true, true, S1, kTileP>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ,
+                                                   sR, stage);
+    else
+        wave_body<K, T, false, false, true, S1, kTileP>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ,
+                                                    sR, stage);
+}
+
 template <int K, typename T>
 hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out, hipStream_t s) {
     const WaveGrid wg = wave_grid(g);
-    const int64_t blocks = (int64_t)wg.nBand * wg.nTile * wg.nChunk;
+    const char* e = getenv("CUSTMA_FWD_TILE");  // benchmarking only: 0 = per-wave kernel
+    const bool tile = g.layout == CUSTMA_LAYOUT_WINDOW && wg.nChunk <= kTileMaxChunks && !(e && atoi(e) == 0);
     prof_begin(PROF_FWD, s);
-    hipLaunchKernelGGL((k_fwd_wave<K, T>), dim3((unsigned)blocks), dim3(64), 0, s, cam, proj, g, sc, sp, out, wg);
+    if (tile) {
+        const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
+        const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
+        // 16-byte stores when every block base is 16-byte aligned: out aligned and
+        // ((t - h_lo) WO + u0) DO = 0 mod 4 for all t (u0 = 0 mod 16)
+        const char* e4 = getenv("CUSTMA_FWD_X4");  // benchmarking only: 0 = dword stores
+        const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0) && !(e4 && atoi(e4) == 0);
+        if (x4)
+            hipLaunchKernelGGL((k_fwd_tile<K, T, true>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
+                               proj, g, sc, sp, out, wg);
+        else
+            hipLaunchKernelGGL((k_fwd_tile<K, T, false>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
+                               proj, g, sc, sp, out, wg);
+    } else {
+        const int64_t blocks = (int64_t)wg.nBand * wg.nTile * wg.nChunk;
+        hipLaunchKernelGGL((k_fwd_wave<K, T>), dim3((unsigned)blocks), dim3(64), 0, s, cam, proj, g, sc, sp, out,
+                           wg);
+    }
     prof_end(PROF_FWD, s);
     return hipGetLastError();
 }

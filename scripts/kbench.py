@@ -3,6 +3,7 @@ import argparse, json, os, sys, time
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import custereomatching_amd as cm
+from custereomatching_amd import _lib
 from bench import synth_pair, EventTimer
 
 CFGS = {
@@ -21,9 +22,13 @@ def run(name, ops, reps):
         for prec in [p for p in ("fast", "exact") if (p == "fast" and "fwd" in ops) or (p == "exact" and "exact" in ops)]:
             out = cm.cost_volume_forward(cam, proj, D, k, lay, prec)
             et = EventTimer()
+            _lib.profile_enable(True)
             for _ in range(reps):
                 et.record(lambda: cm.cost_volume_forward(cam, proj, D, k, lay, prec, out=out))
             ms = et.mean_ms()
+            kms, _ = _lib.profile_mean_ms(_lib.PROF_FWD)
+            _lib.profile_enable(False)
+            res[f"fwd_{prec}_kernel_ms"] = round(kms, 4)
             nb = out.numel() * 4 + 2 * H * W * cam.element_size()
             res[f"fwd_{prec}_ms"] = round(ms, 4)
             res[f"fwd_{prec}_GBps"] = round(nb / ms / 1e6, 1)
