@@ -84,9 +84,7 @@ void carve_stats(const Geo& g, void* ws, Stats* sc, Stats* sp) {
 int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, void* ws, Stats* sc, Stats* sp,
               hipStream_t s) {
     carve_stats(g, ws, sc, sp);
-    int rc = check_hip(launch_stats(cam, dtype, g, *sc, s), "stats(camera)");
-    if (rc) return rc;
-    return check_hip(launch_stats(proj, dtype, g, *sp, s), "stats(projector)");
+    return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s), "stats");
 }
 
 int check_dtype(int32_t dtype) {

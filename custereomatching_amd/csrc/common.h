@@ -217,7 +217,7 @@ __device__ __forceinline__ void st_buf(float v, __amdgpu_buffer_rsrc_t r, uint32
 
 // ---- internal launchers (one translation unit each), called from capi.hip ----
 namespace custma {
-hipError_t launch_stats(const void* img, int dtype, const Geo& g, Stats st, hipStream_t s);
+hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s);
 hipError_t launch_fwd_exact(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             float* out, hipStream_t s);
 hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,

@@ -24,7 +24,11 @@ constexpr int TX = 16, TY = 64, PR = 4;  // 16 x 64 pixels per 256-thread workgr
 // KT > 0: the window size as a compile-time constant (the sweep's instantiations), so the
 // k^2 tap loops unroll and the per-pixel row masks fold away; KT = 0: runtime k.
 template <typename T, int KT>
-__global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g, Stats st) {
+__global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const T* __restrict__ img1, Geo g,
+                                               Stats st0, Stats st1) {
+    // blockIdx.z: 0 = camera, 1 = projector (one launch for both images)
+    const T* __restrict__ img = blockIdx.z ? img1 : img0;
+    const Stats st = blockIdx.z ? st1 : st0;
     extern __shared__ __attribute__((aligned(16))) double lds_d[];
     const int k = KT > 0 ? KT : g.k, r = k / 2, LX = TX + 2 * r, LY = TY + 2 * r;
     double* rs = lds_d;                    // [LY][TX] fp64 k-tap row sums
@@ -57,29 +61,59 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g,
     float m[PR], sq[PR];
 #pragma unroll
     for (int p = 0; p < PR; ++p) { m[p] = 0.f; sq[p] = 0.f; }
+    // Tile rows one at a time (not unrolled: fully unrolled, the compiler keeps all
+    // (k+PR-1) k tile values live across both passes -- 182 VGPRs, 2 waves per SIMD); the
+    // row's k values feed every pixel whose patch holds that row (a wave-uniform branch).
+#pragma unroll 1
+    for (int i2 = 0; i2 < k + PR - 1; ++i2) {
+        float v[KT > 0 ? KT : 1];
+        if constexpr (KT > 0) {
 #pragma unroll
-    for (int i2 = 0; i2 < k + PR - 1; ++i2)
-#pragma unroll
-        for (int j = 0; j < k; ++j) {
-            const float v = t[i2 * LX + j];
-#pragma unroll
-            for (int p = 0; p < PR; ++p)
-                if (i2 - p >= 0 && i2 - p < k) m[p] = m[p] + v;
-        }
-#pragma unroll
-    for (int p = 0; p < PR; ++p) m[p] = m[p] / (float)(k * k);
-#pragma unroll
-    for (int i2 = 0; i2 < k + PR - 1; ++i2)
-#pragma unroll
-        for (int j = 0; j < k; ++j) {
-            const float v = t[i2 * LX + j];
+            for (int j = 0; j < KT; ++j) v[j] = t[i2 * LX + j];
 #pragma unroll
             for (int p = 0; p < PR; ++p)
                 if (i2 - p >= 0 && i2 - p < k) {
-                    const float c = v - m[p];
-                    sq[p] = __builtin_fmaf(c, c, sq[p]);
+#pragma unroll
+                    for (int j = 0; j < KT; ++j) m[p] = m[p] + v[j];
                 }
+        } else {
+            for (int j = 0; j < k; ++j) {
+                const float u = t[i2 * LX + j];
+#pragma unroll
+                for (int p = 0; p < PR; ++p)
+                    if (i2 - p >= 0 && i2 - p < k) m[p] = m[p] + u;
+            }
         }
+    }
+#pragma unroll
+    for (int p = 0; p < PR; ++p) m[p] = m[p] / (float)(k * k);
+#pragma unroll 1
+    for (int i2 = 0; i2 < k + PR - 1; ++i2) {
+        float v[KT > 0 ? KT : 1];
+        if constexpr (KT > 0) {
+#pragma unroll
+            for (int j = 0; j < KT; ++j) v[j] = t[i2 * LX + j];
+#pragma unroll
+            for (int p = 0; p < PR; ++p)
+                if (i2 - p >= 0 && i2 - p < k) {
+#pragma unroll
+                    for (int j = 0; j < KT; ++j) {
+                        const float c = v[j] - m[p];
+                        sq[p] = __builtin_fmaf(c, c, sq[p]);
+                    }
+                }
+        } else {
+            for (int j = 0; j < k; ++j) {
+                const float u = t[i2 * LX + j];
+#pragma unroll
+                for (int p = 0; p < PR; ++p)
+                    if (i2 - p >= 0 && i2 - p < k) {
+                        const float c = u - m[p];
+                        sq[p] = __builtin_fmaf(c, c, sq[p]);
+                    }
+            }
+        }
+    }
     const int64_t x = x0 + lx;
     if (x >= g.W) return;
 #pragma unroll
@@ -103,16 +137,18 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img, Geo g,
 }
 }  // namespace
 
-hipError_t launch_stats(const void* img, int dtype, const Geo& g, Stats st, hipStream_t s) {
-    const dim3 grid((unsigned)cdiv(g.W, TX), (unsigned)cdiv(g.H, TY));
+hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s) {
+    const dim3 grid((unsigned)cdiv(g.W, TX), (unsigned)cdiv(g.H, TY), 2);
     const int LX = TX + 2 * g.r, LY = TY + 2 * g.r;
     const size_t lds = sizeof(double) * 2 * LY * TX + sizeof(float) * LY * LX;
     auto go = [&](auto kc) {
         constexpr int KT = decltype(kc)::value;
         if (dtype == CUSTMA_F16)
-            hipLaunchKernelGGL((k_stats<__half, KT>), grid, dim3(256), lds, s, (const __half*)img, g, st);
+            hipLaunchKernelGGL((k_stats<__half, KT>), grid, dim3(256), lds, s, (const __half*)cam, (const __half*)proj,
+                               g, sc, sp);
         else
-            hipLaunchKernelGGL((k_stats<float, KT>), grid, dim3(256), lds, s, (const float*)img, g, st);
+            hipLaunchKernelGGL((k_stats<float, KT>), grid, dim3(256), lds, s, (const float*)cam, (const float*)proj, g,
+                               sc, sp);
     };
     switch (g.k) {
 #define CUSTMA_K(KK) \
