@@ -13,6 +13,8 @@
 //    bit-identical to argmax of the exact volume.
 #include <float.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "sweep.h"
 
@@ -57,17 +59,35 @@ __global__ __launch_bounds__(256) void k_argmax(const float* __restrict__ vol, i
 
 // Exact reference cost of one voxel (stereo_matching_kernel.cu:39-71, nvcc
 // -fmad=true), using the stats pass's bit-identical means and moments.
-template <typename T>
+// KT > 0: compile-time window; patches fully inside the image take unguarded row loads.
+template <typename T, int KT = 0>
 __device__ float exact_cost(const T* cam, const T* proj, const Geo& g, const Stats& sc, const Stats& sp, int64_t h,
                             int64_t w, int64_t d) {
     const float mc = sc.mean[h * g.W + w], mp = sp.mean[h * g.W + d];
     float e = 0.f;
-    for (int i = 0; i < g.k; ++i)
-        for (int j = 0; j < g.k; ++j) {
-            const float c = ldpad(cam, g.H, g.W, h + i - g.r, w + j - g.r) - mc;
-            const float p = ldpad(proj, g.H, g.W, h + i - g.r, d + j - g.r) - mp;
-            e = __builtin_fmaf(c, p, e);
+    const int k = KT > 0 ? KT : g.k, r = k / 2;
+    if (KT > 0 && h >= r && h + r < g.H && w >= r && w + r < g.W && d >= r && d + r < g.W) {
+        const T* cr = cam + (h - r) * g.W + (w - r);
+        const T* pr = proj + (h - r) * g.W + (d - r);
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+#pragma unroll
+            for (int j = 0; j < k; ++j) {
+                const float c = to_f(cr[j]) - mc;
+                const float p = to_f(pr[j]) - mp;
+                e = __builtin_fmaf(c, p, e);
+            }
+            cr += g.W;
+            pr += g.W;
         }
+    } else {
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j < k; ++j) {
+                const float c = ldpad(cam, g.H, g.W, h + i - r, w + j - r) - mc;
+                const float p = ldpad(proj, g.H, g.W, h + i - r, d + j - r) - mp;
+                e = __builtin_fmaf(c, p, e);
+            }
+    }
     const float den = sqrtf(__builtin_fmaf(sc.sq[h * g.W + w], sp.sq[h * g.W + d], kEps));
     return (e + kEps) / den;
 }
@@ -76,7 +96,7 @@ __device__ __forceinline__ int64_t d_of_s(const Geo& g, int64_t w, int64_t s) {
     return g.layout == CUSTMA_LAYOUT_WINDOW ? w + s : s;
 }
 
-template <typename T>
+template <typename T, int KT>
 __global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                     Stats sc, Stats sp, DispPartial part, int nChunk, float tau,
                                                     int64_t* __restrict__ idx, float* __restrict__ best,
@@ -100,7 +120,7 @@ __global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, c
     const int64_t h = g.h_lo + p / g.WO, w = p % g.WO;
     if (bi != INT64_MAX && (sec == -FLT_MAX || b - sec > tau)) {
         idx[p] = bi;
-        if (best) best[p] = exact_cost(cam, proj, g, sc, sp, h, w, d_of_s(g, w, bi));
+        if (best) best[p] = exact_cost<T, KT>(cam, proj, g, sc, sp, h, w, d_of_s(g, w, bi));
     } else {
         const int32_t slot = atomicAdd(counter, 1);
         queue[slot] = p;
@@ -175,23 +195,39 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
     hipError_t e = hipMemsetAsync(counter, 0, 4, s);
     if (e != hipSuccess) return e;
     // kernel sizes without a sweep instantiation: every pixel is decided exactly
-    const int nChunk = fast_supported(g.k) ? sg.nChunk : 0;
+    // window layout with D + 1 <= 257: the tile kernel reduces all diagonals of a pixel in
+    // one workgroup (one partial per pixel); otherwise per-chunk partials from k_sweep_fwd
+    const bool tile = fast_supported(g.k) && disp_tile_ok(g);
+    const int nChunk = !fast_supported(g.k) ? 0 : tile ? 1 : sg.nChunk;
     if (nChunk) {
-        e = launch_disp_partials(cam, proj, dtype, g, sc, sp, part, s);
+        e = tile ? launch_disp_tile(cam, proj, dtype, g, sc, sp, part, s)
+                 : launch_disp_partials(cam, proj, dtype, g, sc, sp, part, s);
         if (e != hipSuccess) return e;
     }
     // certification margin: 2 x twice the fast path's worst-case error
     const float tau = (float)(8.0 * (g.k * g.k + 6) * 5.9604644775390625e-08);
     const int64_t npix = g.HV() * g.WO;
     const unsigned mb = (unsigned)cdiv(npix, 256);
+    auto merge = [&](auto kc) {
+        constexpr int KT = decltype(kc)::value;
+        if (dtype == CUSTMA_F16)
+            hipLaunchKernelGGL((k_disp_merge<__half, KT>), dim3(mb), dim3(256), 0, s, (const __half*)cam,
+                               (const __half*)proj, g, sc, sp, part, nChunk, tau, idx, best, counter, queue);
+        else
+            hipLaunchKernelGGL((k_disp_merge<float, KT>), dim3(mb), dim3(256), 0, s, (const float*)cam,
+                               (const float*)proj, g, sc, sp, part, nChunk, tau, idx, best, counter, queue);
+    };
+    switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: merge(std::integral_constant<int, KK>{}); break;
+        CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+        default: merge(std::integral_constant<int, 0>{});
+    }
     if (dtype == CUSTMA_F16) {
-        hipLaunchKernelGGL(k_disp_merge<__half>, dim3(mb), dim3(256), 0, s, (const __half*)cam, (const __half*)proj,
-                           g, sc, sp, part, nChunk, tau, idx, best, counter, queue);
         hipLaunchKernelGGL(k_disp_recheck<__half>, dim3(2048), dim3(256), 0, s, (const __half*)cam,
                            (const __half*)proj, g, sc, sp, counter, queue, idx, best);
     } else {
-        hipLaunchKernelGGL(k_disp_merge<float>, dim3(mb), dim3(256), 0, s, (const float*)cam, (const float*)proj, g,
-                           sc, sp, part, nChunk, tau, idx, best, counter, queue);
         hipLaunchKernelGGL(k_disp_recheck<float>, dim3(2048), dim3(256), 0, s, (const float*)cam,
                            (const float*)proj, g, sc, sp, counter, queue, idx, best);
     }

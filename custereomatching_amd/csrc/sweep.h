@@ -163,5 +163,9 @@ inline int64_t sweep_blocks(const SweepGrid& sg) { return (int64_t)sg.nBand * sg
 
 hipError_t launch_disp_partials(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                                 DispPartial part, hipStream_t s);
+// window layout, D + 1 <= 257: the tile kernel writes ONE partial per pixel (all diagonals)
+bool disp_tile_ok(const Geo& g);
+hipError_t launch_disp_tile(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
+                            DispPartial part, hipStream_t s);
 
 }  // namespace custma

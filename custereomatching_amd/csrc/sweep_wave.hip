@@ -22,6 +22,8 @@
 //
 // Per voxel: 2(16+2r)/16 fp64 FMAs + as many ds_read_b64 (row update), 2 fp64
 // adds (column slide), 1 fp64 FMA + cvt (mean correction), fp32 fma + rsq + mul.
+#include <float.h>
+#include <limits.h>
 #include <stdlib.h>
 
 #include <type_traits>
@@ -37,6 +39,7 @@ typedef __attribute__((address_space(3))) volatile double lds_vd;
 typedef __attribute__((address_space(3))) volatile float lds_vf;
 
 constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
+constexpr int kTileMaxChunks = 4;  // k_fwd_tile: diagonal chunks (waves) per workgroup
 
 // REM: this wave (window layout, last chunk, (D+1) % 64 == 1) also computes the single
 // remainder diagonal d0 + 64 = D: lane x < 16 + 2r keeps its column sum, the horizontal box
@@ -48,12 +51,16 @@ constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
 // the whole 16 * DO-float block with dword stores, SS per thread (OOB-masked, so every
 // thread issues exactly SS and the hand-counted vmcnt holds): every volume sector is
 // written once, by one workgroup, in one burst.
-template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2>
+//
+// AMX > 0 (STAGED, fused disparity): no volume; after the barrier each 16-lane group scans
+// one of the 16 LDS rows (all D+1 diagonals of one camera pixel) for (best, second, first
+// index of best), AMX passes of 4 rows per wave, and writes them as one disparity partial.
+template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2, int AMX = 0>
 __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
                                           const Stats& sc, const Stats& sp, float* __restrict__ out,
                                           int64_t u0, int64_t h0, int64_t h1, int64_t d0,
                                           double* rowE, double* rowL, double* sM, float* sQ, double* sR,
-                                          float* stage = nullptr) {
+                                          float* stage = nullptr, DispPartial part = DispPartial{}) {
     constexpr int R = K / 2, NX = TW + 2 * R;
     static_assert(NX + 63 <= kRowP && NX <= 32, "row segment fits the LDS slice and two broadcast registers");
     constexpr uint32_t OOB = 0x80000000u;
@@ -147,7 +154,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     auto compute = [&](Stage& p, int64_t t) {
         // loads(t) were issued at the end of step t-P; after them, for each step s in
         // t-P+1 .. t-1: its stores (from step h0 on) and loads(s+P)
-        constexpr int ST = STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);  // stores per step
+        constexpr int ST = AMX > 0 ? 3 * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);  // stores/step
         static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
 #ifdef CUSTMA_ABL_NOWAIT  // ablation builds only: no wait for the loads (garbage values)
         asm_vmcnt<63>();
@@ -283,7 +290,43 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
                 const int NT = (int)blockDim.x, tid = (int)threadIdx.x;
                 const int total = (int)(nrow * DO);
-                if constexpr (SS < 0) {  // block base 16-byte aligned (checked at launch)
+                if constexpr (AMX > 0) {
+                    const int wv = tid >> 6, nw = NT >> 6, sub = l & 15;
+                    const int64_t prow = (t - g.h_lo) * g.WO + u0;
+                    const uint32_t pb = (uint32_t)(nrow * 4);
+                    const auto rB = make_rsrc(part.best + prow, pb), rS = make_rsrc(part.second + prow, pb);
+                    const auto rI = make_rsrc(part.index + prow, pb);
+#pragma unroll
+                    for (int ps = 0; ps < AMX; ++ps) {
+                        const int m = (ps * nw + wv) * 4 + (l >> 4);  // tile row of this 16-lane group
+                        float b = -FLT_MAX, sec = -FLT_MAX;
+                        int bi = INT_MAX;
+                        // increasing s per lane: the first index wins among equal values
+                        const int mr = m < TW ? m : 0;
+#pragma unroll
+                        for (int i = 0; i < (64 * kTileMaxChunks + 1 + 15) / 16; ++i) {
+                            const int s2 = sub + 16 * i;
+                            if (s2 < (int)DO) {
+                                const float v = sb[mr * DO + s2];
+                                const bool gt = v > b;
+                                sec = gt ? b : fmaxf(sec, v);
+                                bi = gt ? s2 : bi;
+                                b = gt ? v : b;
+                            }
+                        }
+#pragma unroll
+                        for (int off = 8; off > 0; off >>= 1) {
+                            const float ob = __shfl_xor(b, off), os = __shfl_xor(sec, off);
+                            const int oi = __shfl_xor(bi, off);
+                            if (ob > b || (ob == b && oi < bi)) { sec = fmaxf(os, b); b = ob; bi = oi; }
+                            else sec = fmaxf(sec, ob);
+                        }
+                        const uint32_t vo = (sub == 0 && m < TW) ? (uint32_t)(m * 4) : OOB;
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, b), rB, vo, 0u, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, sec), rS, vo, 0u, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32((unsigned int)(bi == INT_MAX ? -1 : bi), rI, vo, 0u, 0);
+                    }
+                } else if constexpr (SS < 0) {  // block base 16-byte aligned (checked at launch)
                     const int n4 = total >> 2;
                     typedef __attribute__((address_space(3))) volatile i32x4 lds_v4;
 #pragma unroll
@@ -364,20 +407,17 @@ __global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, cons
 // Window layout, D + 1 <= 64 * kTileMaxChunks (+1): one workgroup per (column tile, row
 // band) holding all diagonal chunks, wave w = chunk w (the last one also takes the
 // remainder diagonal when wg.rem); outputs leave through the LDS block image (STAGED).
-constexpr int kTileMaxChunks = 4;
 #ifndef CUSTMA_TILE_P
 #define CUSTMA_TILE_P 2
 #endif
 constexpr int kTileP = CUSTMA_TILE_P;  // load pipeline depth (steps)
 constexpr int kWaveLds = (3 * kRowP + 64) * 8 + kRowP * 4;  // rowE, rowL, sM, sR (f64) + sQ (f32)
 
-template <int K, typename T, bool X4>
-#ifndef CUSTMA_TILE_WPE
-#define CUSTMA_TILE_WPE 1
-#endif
-__global__ __launch_bounds__(64 * kTileMaxChunks) __attribute__((amdgpu_waves_per_eu(CUSTMA_TILE_WPE))) void k_fwd_tile(const T* __restrict__ cam,
+template <int K, typename T, bool X4, int AMX = 0>
+__global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __restrict__ cam,
                                                                  const T* __restrict__ proj, Geo g, Stats sc,
-                                                                 Stats sp, float* __restrict__ out, WaveGrid wg) {
+                                                                 Stats sp, float* __restrict__ out, WaveGrid wg,
+                                                                 DispPartial part) {
     extern __shared__ __attribute__((aligned(16))) double lds_t[];
     const int w = (int)(threadIdx.x >> 6);
     char* mine = (char*)lds_t + w * kWaveLds;
@@ -397,14 +437,14 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) __attribute__((amdgpu_waves_pe
     // X4: 4 (5 with rem) 16-byte stores per thread
     constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
     if (!wg.rem)
-        wave_body<K, T, false, false, true, S0, kTileP>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ, sR,
-                                                stage);
+        wave_body<K, T, false, false, true, S0, kTileP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
+                                                             sQ, sR, stage, part);
     else if (w == wg.nChunk - 1)
-        wave_body<K, T, false, true, true, S1, kTileP>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ,
-                                                   sR, stage);
+        wave_body<K, T, false, true, true, S1, kTileP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
+                                                            sQ, sR, stage, part);
     else
-        wave_body<K, T, false, false, true, S1, kTileP>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM, sQ,
-                                                    sR, stage);
+        wave_body<K, T, false, false, true, S1, kTileP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
+                                                             sQ, sR, stage, part);
 }
 
 template <int K, typename T>
@@ -422,10 +462,10 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
         const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0) && !(e4 && atoi(e4) == 0);
         if (x4)
             hipLaunchKernelGGL((k_fwd_tile<K, T, true>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
-                               proj, g, sc, sp, out, wg);
+                               proj, g, sc, sp, out, wg, DispPartial{});
         else
             hipLaunchKernelGGL((k_fwd_tile<K, T, false>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
-                               proj, g, sc, sp, out, wg);
+                               proj, g, sc, sp, out, wg, DispPartial{});
     } else {
         const int64_t blocks = (int64_t)wg.nBand * wg.nTile * wg.nChunk;
         hipLaunchKernelGGL((k_fwd_wave<K, T>), dim3((unsigned)blocks), dim3(64), 0, s, cam, proj, g, sc, sp, out,
@@ -433,6 +473,38 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
     }
     prof_end(PROF_FWD, s);
     return hipGetLastError();
+}
+
+// Fused disparity through the tile kernel (window layout, D + 1 <= 257): one partial per pixel.
+template <int K, typename T>
+hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, DispPartial part, hipStream_t s) {
+    const WaveGrid wg = wave_grid(g);
+    const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
+    const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
+    prof_begin(PROF_FWD, s);
+    if (wg.nChunk == 4)
+        hipLaunchKernelGGL((k_fwd_tile<K, T, false, 1>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
+                           proj, g, sc, sp, nullptr, wg, part);
+    else if (wg.nChunk >= 2)
+        hipLaunchKernelGGL((k_fwd_tile<K, T, false, 2>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
+                           proj, g, sc, sp, nullptr, wg, part);
+    else
+        hipLaunchKernelGGL((k_fwd_tile<K, T, false, 4>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
+                           proj, g, sc, sp, nullptr, wg, part);
+    prof_end(PROF_FWD, s);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t dispatch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, DispPartial part,
+                        hipStream_t s) {
+    switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: return launch_amx<KK, T>(cam, proj, g, sc, sp, part, s);
+        CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+        default: return hipErrorInvalidValue;
+    }
 }
 
 template <typename T>
@@ -464,6 +536,17 @@ WaveGrid wave_grid(const Geo& g) {
     while (wg.TH > 8 && (int64_t)wg.nTile * wg.nChunk * cdiv(g.HV(), wg.TH) < 8192) wg.TH /= 2;
     wg.nBand = (int)cdiv(g.HV(), wg.TH);
     return wg;
+}
+
+bool disp_tile_ok(const Geo& g) {
+    const char* e = getenv("CUSTMA_FWD_TILE");  // benchmarking only: 0 = the LDS-form partials
+    return g.layout == CUSTMA_LAYOUT_WINDOW && wave_grid(g).nChunk <= kTileMaxChunks && !(e && atoi(e) == 0);
+}
+
+hipError_t launch_disp_tile(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
+                            DispPartial part, hipStream_t s) {
+    if (dtype == CUSTMA_F16) return dispatch_amx((const __half*)cam, (const __half*)proj, g, sc, sp, part, s);
+    return dispatch_amx((const float*)cam, (const float*)proj, g, sc, sp, part, s);
 }
 
 hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,

@@ -171,6 +171,28 @@ def test_disparity_certified_bit_identical(gpu, case, layout):
         assert int(nre.item()) > 0  # ties everywhere: the exact re-decision ran
 
 
+DISP_TILE_CASES = [
+    # window layout, fused disparity through the tile kernel: 1, 2 (+remainder), 3 and 4 (+remainder)
+    # diagonal chunks per workgroup
+    (18, 150, 5, 90, "textured"),
+    (24, 300, 9, 128, "quantized"),
+    (20, 200, 7, 150, "smooth"),
+    (20, 320, 11, 256, "textured"),
+]
+
+
+@pytest.mark.parametrize("case", DISP_TILE_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_D{c[3]}" for c in DISP_TILE_CASES])
+def test_disparity_window_tile(gpu, case):
+    H, W, k, D, kind = case
+    cam, proj = make_pair(H, W, D, seed=23, kind=kind)
+    ref = O.forward(cam, proj, k, layout=O.WINDOW, D=D, contract=1)
+    ridx, rbest = O.argmax(ref)
+    idx, best = cm.stereo_disparity(_dev(cam, gpu), _dev(proj, gpu), D, k, WIN)
+    idx, best = idx.cpu().numpy(), best.cpu().numpy()
+    assert np.array_equal(idx, ridx), f"{np.count_nonzero(idx != ridx)} pixels differ"
+    assert np.array_equal(best.view(np.uint32), rbest.view(np.uint32))
+
+
 def _rand_grad(shape, seed):
     return np.random.default_rng(seed).standard_normal(shape).astype(np.float32)
 
