@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libcustma_hip.so")
-SOURCES = ["capi.hip", "stats.hip", "fwd_exact.hip", "sweep_fwd.hip", "sweep_wave.hip", "bwd_fused.hip", "select.hip"]
+SOURCES = ["capi.hip", "stats.hip", "fwd_exact.hip", "sweep_fwd.hip", "sweep_wave.hip", "bwd_fused.hip", "select.hip", "preprocess.hip"]
 ARCH = os.environ.get("CUSTMA_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: fused multiply-adds only where written (__builtin_fmaf / fma);

@@ -266,6 +266,20 @@ int custma_backward_band(const float* grad, const float* cost_volume, const void
                      "backward");
 }
 
+int custma_image_u8_to_unit(const uint8_t* image, int64_t H, int64_t W, int32_t channels, int32_t channel,
+                            int32_t out_dtype, void* out, void* stream) {
+    if (H < 0 || W < 0) return fail(CUSTMA_E_ARG, "negative image size");
+    if (channels < 1) return fail(CUSTMA_E_ARG, "channels must be >= 1 (got %d)", channels);
+    if (channel < 0 || channel >= channels)
+        return fail(CUSTMA_E_ARG, "channel %d out of range for %d channels", channel, channels);
+    int rc = check_dtype(out_dtype);
+    if (rc) return rc;
+    if (H == 0 || W == 0) return CUSTMA_OK;
+    if (!image || !out) return fail(CUSTMA_E_NULL, "null pointer argument");
+    return check_hip(launch_u8_to_unit(image, H * W, channels, channel, out_dtype, out, (hipStream_t)stream),
+                     "image_u8_to_unit");
+}
+
 int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, float* best, void* stream) {
     if (rows < 0 || n < 0) return fail(CUSTMA_E_ARG, "negative size");
     if (rows == 0) return CUSTMA_OK;

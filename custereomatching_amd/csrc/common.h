@@ -217,6 +217,8 @@ __device__ __forceinline__ void st_buf(float v, __amdgpu_buffer_rsrc_t r, uint32
 
 // ---- internal launchers (one translation unit each), called from capi.hip ----
 namespace custma {
+hipError_t launch_u8_to_unit(const uint8_t* src, int64_t npix, int C, int ch, int out_dtype, void* out,
+                             hipStream_t s);
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s);
 hipError_t launch_fwd_exact(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             float* out, hipStream_t s);

@@ -111,6 +111,14 @@ int custma_disparity_band(const void* camera, const void* projector, int32_t dty
 int custma_profile_enable(int32_t on);
 int custma_profile_mean_ms(int32_t which, float* ms, int32_t* count);
 
+/* Image preprocessing before the path (examples/verify.py:138-142, 148): an 8-bit image [H][W][channels]
+ * (interleaved, as cv2.imread returns it; channels = 1 for grayscale) -> out[H][W] = image[.][.][channel] / 255,
+ * computed as numpy does (float64 division, rounded once to float32; out_dtype CUSTMA_F16 rounds that float32
+ * to float16).  Replaces the host-side `np.array(cv2.imread(...)) / 255` + `torch.tensor(..., float32).cuda()`
+ * + `rgb[:, :, 0]` of the reference's driver with one HBM pass on the device. */
+int custma_image_u8_to_unit(const uint8_t* image, int64_t H, int64_t W, int32_t channels, int32_t channel,
+                            int32_t out_dtype, void* out, void* stream);
+
 /* First-index argmax over the last axis of a [rows, n] fp32 array (torch.argmax semantics), as the
  * reference's callers do on the volume (examples/verify.py:72, examples/test.py:78-83). */
 int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, float* best, void* stream);

@@ -142,3 +142,13 @@ def cost_error_bound(k: int) -> float:
     """
     u = 2.0 ** -24
     return (k * k + 6) * u
+
+
+def image_u8_to_unit(image, channel=0, dtype=np.float32):
+    """The reference driver's preprocessing (examples/verify.py:138-142, 148):
+    ``np.array(cv2.imread(...)) / 255`` (numpy float64 true division), then
+    ``torch.tensor(..., dtype=float32)`` and the camera channel ``[:, :, 0]``."""
+    img = np.asarray(image)
+    if img.ndim == 3:
+        img = img[:, :, channel]
+    return (img / 255).astype(dtype)
