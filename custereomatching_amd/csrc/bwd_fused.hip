@@ -444,7 +444,13 @@ __global__ __launch_bounds__(64) void k_bwd_sweep(Geo g, BwdArgs a) {
 // column's Y is not needed at all.
 constexpr int NWC = 4;          // waves per cooperative workgroup
 constexpr int TRW = TRB / NWC;  // own rows per wave
-constexpr int FBC = 8;          // steps per flush (small buffers: 3 workgroups per CU at k = 9)
+#ifndef CUSTMA_BWD_DEPTH
+#define CUSTMA_BWD_DEPTH 1  // 2 measured no faster (C2 full 5.37 vs 5.19 ms): latency is not the limit
+#endif
+constexpr int BDP = CUSTMA_BWD_DEPTH;  // steps of loads in flight (1 or 2)
+// steps per flush (small buffers: 3 workgroups per CU at k = 9); a multiple of BDP + 1, so
+// every flush block starts on load buffer 0
+constexpr int FBC = BDP == 2 ? 6 : 8;
 
 // Finish 3 registers (each already summed over the 4 lanes {l, l+16, l+32, l+48}, one
 // value per 16-lane row): afterwards every lane holds the full 64-lane sum of one of the 12.
@@ -522,10 +528,11 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         return make_rsrc(a.part + ((size_t)t * a.S + slot) * plane + (size_t)(y0 + yw) * g.W, prow_bytes);
     };
     auto flush = [&](int wfirst, int nsteps) {
+        if constexpr (BDP == 2) asm_vmcnt<TRW * 5 + (HPW > 0 ? HPW : 1) * 2 + 4>();  // all but the newest issue
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        // lanes 0-31: step jcol, own row m (the upper half idles)
-        const int jcol = ln & (FBC - 1), m = (ln / FBC) & 3;
+        // lanes 0..4 FBC-1: step jcol, own row m (the rest idle)
+        const int jcol = ln % FBC, m = (ln / FBC) & 3;
         const bool live = jcol < nsteps && ln < 4 * FBC;
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
@@ -617,11 +624,21 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
 
     int sidx = 0;  // ring slot of the current step (step count mod K)
-    auto step = [&](Ld& cur, Ld& nxt, int w, int s) {
-        // the only vector-memory operations since cur was issued: a flush's stores
-        asm_vmcnt<0>();
+    // loads per issue() (asm_ld5s / asm_ld2s / asm_ld4) and stores per flush(), per thread
+    constexpr int NL = TRW * 5 + HP * 2 + 4, SF = 6;
+    static_assert(NL + SF <= 63, "vmcnt holds the pipeline");
+    // cur was issued BDP steps ago; issued since: the later steps' loads, and a flush's SF
+    // stores after step s = FBC-1 of the previous block (flush() itself waits until only
+    // the newest issue is in flight: at s = 0 of a block after a flush cur has landed)
+    auto step = [&](Ld& cur, Ld& nxt, int w, int s, bool flushed) {
+        if constexpr (BDP == 2) {
+            if (!flushed || s >= 2) asm_vmcnt<NL>();
+            else if (s == 1) asm_vmcnt<NL + SF>();
+        } else {
+            asm_vmcnt<0>();
+        }
         tie(cur);
-        issue(w + 1, nxt);  // past the segment's end: harmless, drained before the wave ends
+        issue(w + BDP, nxt);  // past the segment's end: harmless, drained before the wave ends
         float* Acur = Abuf + ((w - w0) & 1) * (NY * 64);
         if (lane == 0) {
 #pragma unroll
@@ -689,22 +706,34 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         cbuf[s][qlane] = reduce_tail3(w0r, w1r, w2r, lane);
     };
 
-    Ld L[2];
+    Ld L[BDP + 1];
     issue(w0, L[0]);
+    if constexpr (BDP == 2) issue(w0 + 1, L[1]);
     for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
-        const int nsteps = min(FBC, wend - wfirst);  // FBC is even: every block starts on L[0]
-        for (int s = 0; s < nsteps; s += 2) {
-            step(L[0], L[1], wfirst + s, s);
-            if (s + 1 >= nsteps) break;
-            step(L[1], L[0], wfirst + s + 1, s + 1);
+        const int nsteps = min(FBC, wend - wfirst);  // FBC = a multiple of BDP + 1: blocks start on L[0]
+        const bool fl = wfirst > w0;
+        if constexpr (BDP == 2) {
+            for (int s = 0; s < nsteps; s += 3) {
+                step(L[0], L[2], wfirst + s, s, fl);
+                if (s + 1 >= nsteps) break;
+                step(L[1], L[0], wfirst + s + 1, s + 1, fl);
+                if (s + 2 >= nsteps) break;
+                step(L[2], L[1], wfirst + s + 2, s + 2, fl);
+            }
+        } else {
+            for (int s = 0; s < nsteps; s += 2) {
+                step(L[0], L[1], wfirst + s, s, fl);
+                if (s + 1 >= nsteps) break;
+                step(L[1], L[0], wfirst + s + 1, s + 1, fl);
+            }
         }
         flush(wfirst, nsteps);
     }
-    // The last step's prefetch is still in flight: keep its registers live (the compiler would
-    // otherwise reuse them in the last flush) until it has landed.
+    // The last steps' prefetches are still in flight: keep their registers live (the compiler
+    // would otherwise reuse them in the last flush) until they have landed.
     asm_vmcnt<0>();
-    tie(L[0]);
-    tie(L[1]);
+#pragma unroll
+    for (int i = 0; i <= BDP; ++i) tie(L[i]);
     // ---- final projector state: lane l holds column (wend - 1) + off + d0 + l
 #pragma unroll
     for (int t = 0; t < 3; ++t) {

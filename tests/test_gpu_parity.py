@@ -207,6 +207,9 @@ BWD_CASES = [
     (22, 50, 15, 30, "textured"),
     (24, 48, 3, 0, "textured"),
     (24, 48, 5, 16, "constant"),
+    # many steps per segment: several flush blocks of the backward's load pipeline
+    (36, 200, 11, 60, "textured"),
+    (34, 260, 9, 100, "smooth"),
 ]
 
 
