@@ -862,18 +862,35 @@ __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict
         tM[e] = ok ? MB[q] : 0.0;
     }
     __syncthreads();
+    // separable box (fixed order, deterministic): k-tap row sums of the L x TS columns the
+    // tile's outputs need, then k-tap column sums -- 2k adds per output instead of k^2
+    double* hA = tM + L * L;
+    double* hB = hA + L * TS;
+    double* hM = hB + L * TS;
+    for (int e = threadIdx.x; e < L * TS; e += 256) {
+        const int ry = e / TS, cx = e % TS;
+        double a = 0, b = 0, m = 0;
+        for (int jx = 0; jx < g.k; ++jx) {
+            const int f = ry * L + cx + jx;
+            a += tA[f];
+            b += tB[f];
+            m += tM[f];
+        }
+        hA[e] = a;
+        hB[e] = b;
+        hM[e] = m;
+    }
+    __syncthreads();
     const int ly = threadIdx.x / TS, lx = threadIdx.x % TS;
     const int64_t y = y0 + ly, x = x0 + lx;
     if (y >= g.H || x >= g.W) return;
-    // separable box: rows first (k column sums per thread would re-read; k^2 adds is fine here)
     double sa = 0, sb = 0, sm = 0;
-    for (int i = 0; i < g.k; ++i)
-        for (int jx = 0; jx < g.k; ++jx) {
-            const int e = (ly + i) * L + lx + jx;
-            sa += tA[e];
-            sb += tB[e];
-            sm += tM[e];
-        }
+    for (int i = 0; i < g.k; ++i) {
+        const int e = (ly + i) * TS + lx;
+        sa += hA[e];
+        sb += hB[e];
+        sm += hM[e];
+    }
     const int64_t q = y * g.W + x;
     const double ip = (double)to_f(img[q]) - (double)shift[side];
     out[q] = (float)(T1[q] - sa - ip * sb + sm);
@@ -1049,7 +1066,7 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc);
     const int L = 16 + 2 * g.r;
     hipLaunchKernelGGL(k_bwd_combine2<T>, dim3((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2), dim3(256),
-                       sizeof(double) * 3 * L * L, s, g, cam, proj, shift, acc, dcam, dproj);
+                       sizeof(double) * 3 * (L * L + L * 16), s, g, cam, proj, shift, acc, dcam, dproj);
     return hipGetLastError();
 }
 
