@@ -448,6 +448,15 @@ constexpr int TRW = TRB / NWC;  // own rows per wave
 #define CUSTMA_BWD_DEPTH 1  // 2 measured no faster (C2 full 5.37 vs 5.19 ms): latency is not the limit
 #endif
 constexpr int BDP = CUSTMA_BWD_DEPTH;  // steps of loads in flight (1 or 2)
+#ifndef CUSTMA_BWD_SLIDE
+#define CUSTMA_BWD_SLIDE 1
+#endif
+// Sliding projector-side columns: the per-voxel projector values Y, mp', p' of a lane at
+// column w + dl are the next lane's values of the previous step, so they move down one
+// lane per step (DPP wave_shl:1) and only lane 63 takes a new column, read from a register
+// loaded once per 64 steps -- instead of a 64-lane load of each per step (those image rows
+// do not stay in L2 beside the gradient stream: ~half of the kernel's L2 misses).
+constexpr bool SLIDE = CUSTMA_BWD_SLIDE && BDP == 1;
 // steps per flush (small buffers: 3 workgroups per CU at k = 9); a multiple of BDP + 1, so
 // every flush block starts on load buffer 0
 constexpr int FBC = BDP == 2 ? 6 : 8;
@@ -599,33 +608,73 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         const bool ve = w >= lwlo && w < lwhi;
         const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
         const uint32_t oYe = col_off(w + dl), oPq = col_off(xb + dl);
+        if constexpr (SLIDE) {
 #pragma unroll
-        for (int m = 0; m < TRW; ++m)
-            asm_ld5s(b.ge[m], b.cv[m], b.Ye[m], b.mp[m], b.pq[m], oGe, oYe, oPq, dG, dV, dY, dM, dP, sVo[m], sIo[m]);
+            for (int m = 0; m < TRW; ++m) asm_ld2s(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
 #pragma unroll
-        for (int i = 0; i < HP; ++i) {
-            const bool ok = wv + NWC * i < NH;
-            asm_ld2s(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dY, sVh[i], sIh[i]);
+            for (int i = 0; i < HP; ++i) asm_ld1s(b.hg[i], wv + NWC * i < NH ? oGe : kOOB, dG, sVh[i]);
+        } else {
+#pragma unroll
+            for (int m = 0; m < TRW; ++m)
+                asm_ld5s(b.ge[m], b.cv[m], b.Ye[m], b.mp[m], b.pq[m], oGe, oYe, oPq, dG, dV, dY, dM, dP, sVo[m],
+                         sIo[m]);
+#pragma unroll
+            for (int i = 0; i < HP; ++i) {
+                const bool ok = wv + NWC * i < NH;
+                asm_ld2s(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dY, sVh[i], sIh[i]);
+            }
         }
         const int r16 = lane & 15;
         asm_ld4(b.x0, b.x1, b.mc, b.cx, r16 < NY ? img_off((int)ir0 + r16, w) : kOOB,
                 16 + r16 < NY ? img_off((int)ir0 + 16 + r16, w) : kOOB, img_off(y0i + yw + (lane & 3), w),
                 img_off(y0i + yw + (lane & 3), xb), dX, dMc, dCc);
     };
+    // SLIDE: the current step's projector-side columns (lane l: column w + dl, p': w - R + dl)
+    // and the once-per-64-steps column block whose lane i feeds lane 63 at step w0 + 1 + 64k + i
+    uint32_t sY[TRW], sMp[TRW], sPq[TRW], shY[HP], bY[TRW], bMp[TRW], bPq[TRW], bhY[HP];
+    auto load_cols = [&](uint32_t* Y, uint32_t* Mp, uint32_t* Pq, uint32_t* hY, int cb) {
+        const uint32_t oY = col_off(cb + dl), oP = col_off(cb - R + dl);
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) {
+            asm_ld2s(Y[m], Mp[m], oY, oY, dY, dM, sIo[m], sIo[m]);
+            asm_ld1s(Pq[m], oP, dP, sIo[m]);
+        }
+#pragma unroll
+        for (int i = 0; i < HP; ++i) asm_ld1s(hY[i], wv + NWC * i < NH ? oY : kOOB, dY, sIh[i]);
+    };
+    auto tie_cols = [&]() {
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) {
+            asm_tie(sY[m]); asm_tie(sMp[m]); asm_tie(sPq[m]); asm_tie(bY[m]); asm_tie(bMp[m]); asm_tie(bPq[m]);
+        }
+#pragma unroll
+        for (int i = 0; i < HP; ++i) { asm_tie(shY[i]); asm_tie(bhY[i]); }
+    };
+    auto slide1 = [&](uint32_t v, uint32_t b, int idx) -> uint32_t {
+        int sh = __builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);  // lane l <- v[l+1]
+        const int nv = __builtin_amdgcn_readlane((int)b, idx);
+        asm volatile("v_writelane_b32 %0, %1, 63" : "+v"(sh) : "s"(nv));
+        return (uint32_t)sh;
+    };
     auto tie = [&](Ld& b) {
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
-            asm_tie(b.ge[m]); asm_tie(b.cv[m]); asm_tie(b.Ye[m]); asm_tie(b.mp[m]); asm_tie(b.pq[m]);
+            asm_tie(b.ge[m]); asm_tie(b.cv[m]);
+            if constexpr (!SLIDE) { asm_tie(b.Ye[m]); asm_tie(b.mp[m]); asm_tie(b.pq[m]); }
         }
 #pragma unroll
-        for (int i = 0; i < HP; ++i) { asm_tie(b.hg[i]); asm_tie(b.hY[i]); }
+        for (int i = 0; i < HP; ++i) {
+            asm_tie(b.hg[i]);
+            if constexpr (!SLIDE) asm_tie(b.hY[i]);
+        }
         asm_tie(b.x0); asm_tie(b.x1); asm_tie(b.mc); asm_tie(b.cx);
+        if constexpr (SLIDE) tie_cols();
     };
     auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
 
     int sidx = 0;  // ring slot of the current step (step count mod K)
     // loads per issue() (asm_ld5s / asm_ld2s / asm_ld4) and stores per flush(), per thread
-    constexpr int NL = TRW * 5 + HP * 2 + 4, SF = 6;
+    constexpr int NL = (SLIDE ? TRW * 2 + HP : TRW * 5 + HP * 2) + 4, SF = 6;
     static_assert(NL + SF <= 63, "vmcnt holds the pipeline");
     // cur was issued BDP steps ago; issued since: the later steps' loads, and a flush's SF
     // stores after step s = FBC-1 of the previous block (flush() itself waits until only
@@ -638,6 +687,22 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             asm_vmcnt<0>();
         }
         tie(cur);
+        if constexpr (SLIDE) {
+            if (w > w0) {  // move the columns down one lane; lane 63 takes column w + 63 (+ offset)
+                const int idx = (w - w0 - 1) & 63;
+#pragma unroll
+                for (int m = 0; m < TRW; ++m) {
+                    sY[m] = slide1(sY[m], bY[m], idx);
+                    sMp[m] = slide1(sMp[m], bMp[m], idx);
+                    sPq[m] = slide1(sPq[m], bPq[m], idx);
+                }
+#pragma unroll
+                for (int i = 0; i < HP; ++i) shY[i] = slide1(shY[i], bhY[i], idx);
+            }
+            // the block for steps w + 1 .. w + 64 (lane i -> step w + 1 + i): columns w + 64 + i (+ offset);
+            // issued after this step's reads of the previous block
+            if (((w - w0) & 63) == 0) load_cols(bY, bMp, bPq, bhY, w + 64);
+        }
         issue(w + BDP, nxt);  // past the segment's end: harmless, drained before the wave ends
         float* Acur = Abuf + ((w - w0) & 1) * (NY * 64);
         if (lane == 0) {
@@ -660,12 +725,12 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
             const int y = R + yw + m;
-            const float Xf = xrow(y), Ye = F(cur.Ye[m]);
+            const float Xf = xrow(y), Ye = F(SLIDE ? sY[m] : cur.Ye[m]);
             const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, Ye, kEps));
             const float Ae = F(cur.ge[m]) * rSe;
             Acur[y * 64 + lane] = Ae;
             const float V = Ae * F(cur.cv[m]) * rSe;
-            amv[m] = Ae * F(cur.mp[m]);
+            amv[m] = Ae * F(SLIDE ? sMp[m] : cur.mp[m]);
             bv[m] = V * Ye;
             const float mcm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mco), m));
             P[1][m] = shl1_add(P[1][m], Ae * mcm);
@@ -677,7 +742,8 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             if (q < NH) {
                 const int y = halo_row(q);
                 const float Xf = xrow(y);
-                Acur[y * 64 + lane] = F(cur.hg[i]) * __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, F(cur.hY[i]), kEps));
+                Acur[y * 64 + lane] =
+                    F(cur.hg[i]) * __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, F(SLIDE ? shY[i] : cur.hY[i]), kEps));
             }
         }
         __syncthreads();  // the unit's A rows of this step are published
@@ -695,7 +761,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             float* rs = ring + (sidx * TRW + m) * 64 + lane;  // V of row m, K steps ago
             HV[m] += v - *rs;
             *rs = v;
-            t1v[m] = (F(cur.pq[m]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
+            t1v[m] = (F(SLIDE ? sPq[m] : cur.pq[m]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
             const float cxm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxo), m));
             P[0][m] = shl1_add(P[0][m], cxm * HV[m]);
         }
@@ -707,6 +773,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     };
 
     Ld L[BDP + 1];
+    if constexpr (SLIDE) load_cols(sY, sMp, sPq, shY, w0);  // the first step's columns, all lanes
     issue(w0, L[0]);
     if constexpr (BDP == 2) issue(w0 + 1, L[1]);
     for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
@@ -734,6 +801,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     asm_vmcnt<0>();
 #pragma unroll
     for (int i = 0; i <= BDP; ++i) tie(L[i]);
+    if constexpr (SLIDE) tie_cols();
     // ---- final projector state: lane l holds column (wend - 1) + off + d0 + l
 #pragma unroll
     for (int t = 0; t < 3; ++t) {

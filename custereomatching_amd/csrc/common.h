@@ -155,6 +155,13 @@ __device__ __forceinline__ void asm_ld2s(uint32_t& a0, uint32_t& a1, uint32_t oA
         : "=&v"(a0), "=&v"(a1)
         : "v"(oA), "v"(oB), "s"(r0), "s"(r1), "s"(sA), "s"(sB));
 }
+__device__ __forceinline__ void asm_ld1s(uint32_t& a0, uint32_t oA, i32x4 r0, uint32_t sA) {
+    asm volatile(
+        "s_nop 4\n\t"
+        "buffer_load_dword %0, %1, %2, %3 offen"
+        : "=&v"(a0)
+        : "v"(oA), "s"(r0), "s"(sA));
+}
 __device__ __forceinline__ void asm_ld4(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t oA,
                                         uint32_t oB, uint32_t oC, uint32_t oD, i32x4 r0, i32x4 r1, i32x4 r2) {
     asm volatile(
