@@ -448,6 +448,9 @@ constexpr int TRW = TRB / NWC;  // own rows per wave
 #define CUSTMA_BWD_DEPTH 1  // 2 measured no faster (C2 full 5.37 vs 5.19 ms): latency is not the limit
 #endif
 constexpr int BDP = CUSTMA_BWD_DEPTH;  // steps of loads in flight (1 or 2)
+#ifndef CUSTMA_BWD_ORDER
+#define CUSTMA_BWD_ORDER 1
+#endif
 #ifndef CUSTMA_BWD_SLIDE
 #define CUSTMA_BWD_SLIDE 1
 #endif
@@ -815,14 +818,24 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 
 template <int K>
 __global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
-    // same unit order as k_bwd_sweep (one workgroup per unit)
+    // XCD x owns row groups [x nRGx, (x+1) nRGx) (their halo rows are read on one XCD).
+    // CUSTMA_BWD_ORDER 1 (default): units segment-major, chunk rank minor, so the workgroups
+    // resident on an XCD at once hold adjacent diagonal chunks of one column segment: a wave's
+    // 256-byte gradient / volume row segment spans three 128-byte lines whose outer parts the
+    // neighbouring chunk's workgroup reads at the same step (L2 hits instead of a second fetch).
+    // 0: chunk-major (k_bwd_sweep's order).
     const int64_t hb = blockIdx.x, xi = hb / 8, x = hb % 8;
     const int nRGx = (a.nRG + 7) / 8;
     const int64_t unit = xi / nRGx;
     const int rg = (int)(x * nRGx + xi % nRGx);
     if (rg >= a.nRG || unit >= (int64_t)a.nChunk * a.nsegMax) return;
+#if CUSTMA_BWD_ORDER
+    const int j = chunk_of_rank((int)(unit % a.nChunk), a.nChunk, a.jc);
+    const int sg = (int)(unit / a.nChunk);
+#else
     const int j = chunk_of_rank((int)(unit / a.nsegMax), a.nChunk, a.jc);
     const int sg = (int)(unit % a.nsegMax);
+#endif
     if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
     constexpr int NY = TRB + 2 * (K / 2);
     __shared__ __attribute__((aligned(16))) float Abuf[2 * NY * 64];

@@ -10,7 +10,7 @@ VARIANTS = {"nostore": ["CUSTMA_ABL_NOSTORE"], "noupdate": ["CUSTMA_ABL_NOUPDATE
             "aux3": ["CUSTMA_STORE_AUX=3"], "aux17": ["CUSTMA_STORE_AUX=17"], "aux18": ["CUSTMA_STORE_AUX=18"],
             "aux19": ["CUSTMA_STORE_AUX=19"],
             "nowait": ["CUSTMA_ABL_NOWAIT"], "so_nowait": ["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT", "CUSTMA_ABL_NOWAIT"],
-            "tilep2": ["CUSTMA_TILE_P=2"], "stats7": ["CUSTMA_ABL_STATS7"],
+            "tilep2": ["CUSTMA_TILE_P=2"], "border0": ["CUSTMA_BWD_ORDER=0"], "stats7": ["CUSTMA_ABL_STATS7"],
             "so_stats7": ["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT", "CUSTMA_ABL_STATS7"],
             "bnoleave": ["CUSTMA_ABL_NOLEAVE"], "bnoimg": ["CUSTMA_ABL_NOIMG"], "bnored": ["CUSTMA_ABL_NORED"],
             "pf4": ["CUSTMA_BWD_PF=4"], "pf8": ["CUSTMA_BWD_PF=8"], "pf16": ["CUSTMA_BWD_PF=16"],
