@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libcustma_hip.so")
-SOURCES = ["capi.hip", "stats.hip", "fwd_exact.hip", "sweep_fwd.hip", "sweep_wave.hip", "bwd_fused.hip", "select.hip", "preprocess.hip"]
+SOURCES = ["capi.hip", "stats.hip", "fwd_exact.hip", "sweep_fwd.hip", "sweep_wave.hip", "bwd_fused.hip", "bwd_generic.hip", "select.hip", "preprocess.hip"]
 ARCH = os.environ.get("CUSTMA_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: fused multiply-adds only where written (__builtin_fmaf / fma);
@@ -42,13 +42,29 @@ def _compile(src, extra=(), libdir=LIBDIR):
     return out
 
 
+def _headers():
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [
+        os.path.join(HERE, "..", "include", "custma.h")]
+
+
+def _stale(src, hdr_mtime):
+    o = _obj(src)
+    if not os.path.exists(o):
+        return True
+    return os.path.getmtime(o) < max(hdr_mtime, os.path.getmtime(os.path.join(CSRC, src)))
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Incremental: a translation unit is recompiled when it or any header is newer than its object."""
     os.makedirs(LIBDIR, exist_ok=True)
     newest = max(os.path.getmtime(p) for p in _deps())
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
         return LIB
-    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
-        objs = list(ex.map(_compile, SOURCES))
+    hdr = max(os.path.getmtime(p) for p in _headers())
+    todo = [s for s in SOURCES if force or _stale(s, hdr)]
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(len(todo), os.cpu_count() or 4))) as ex:
+        list(ex.map(_compile, todo))
+    objs = [_obj(s) for s in SOURCES]
     cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

@@ -39,6 +39,10 @@
 // emitted every step.  Both go through a 16-step LDS buffer to coalesced
 // stores of fp32 partial sums per diagonal chunk; k_bwd_gather sums the
 // chunks and k_bwd_combine applies the box filters.
+#include <algorithm>
+#include <utility>
+#include <vector>
+
 #include "common.h"
 #include "sweep.h"
 #include "xlane.h"
@@ -1032,6 +1036,7 @@ constexpr int kSumBlocks = 512;
 
 struct BwdPlan {
     int nChunk, S, Sj, nRG, jc, nsegMax;
+    bool ok;
     int64_t dlo, ylo, yhi;
     size_t part_bytes, acc_bytes, cover_bytes, prep_bytes, misc_bytes;
 };
@@ -1050,28 +1055,34 @@ BwdPlan plan_bwd(const Geo& g) {
         p.jc = (int)(jc < 0 ? 0 : jc >= p.nChunk ? p.nChunk - 1 : jc);
     }
     // slots: 2 x the max number of chunks covering one column over the four range classes
-    // (segment parity separates the overlapping projector ranges of adjacent segments)
+    // (segment parity separates the overlapping projector ranges of adjacent segments): max
+    // interval overlap by a sweep over the sorted range ends.  An allocation failure leaves
+    // p.ok false, which backward_supported() reports (never a silently undersized S).
     p.S = 1;
-    {
+    p.ok = true;
+    try {
         const int64_t W = g.W;
-        int64_t* diff = (int64_t*)calloc((size_t)(W + 1), sizeof(int64_t));
         const int ts[4] = {0, 1, 3, 4};
-        for (int c = 0; c < 4 && diff; ++c) {
-            for (int64_t x = 0; x <= W; ++x) diff[x] = 0;
+        std::vector<std::pair<int64_t, int>> ev;
+        ev.reserve(2 * (size_t)p.nChunk);
+        for (int c = 0; c < 4; ++c) {
+            ev.clear();
             for (int j = 0; j < p.nChunk; ++j) {
                 int64_t lo, hi;
                 type_range(chunk_geo(g, p.dlo, j), r, ts[c], &lo, &hi);
                 lo = lo < 0 ? 0 : lo;
                 hi = hi > W ? W : hi;
-                if (lo < hi) { diff[lo] += 1; diff[hi] -= 1; }
+                if (lo < hi) { ev.emplace_back(lo, 1); ev.emplace_back(hi, -1); }
             }
-            int64_t run = 0;
-            for (int64_t x = 0; x < W; ++x) {
-                run += diff[x];
-                if (run > p.S) p.S = (int)run;
+            std::sort(ev.begin(), ev.end());  // at equal positions the -1 (range end) comes first
+            int run = 0;
+            for (const auto& e : ev) {
+                run += e.second;
+                if (run > p.S) p.S = run;
             }
         }
-        free(diff);
+    } catch (...) {
+        p.ok = false;
     }
     p.Sj = p.S;
     p.S = 2 * p.Sj;
@@ -1161,6 +1172,7 @@ size_t backward_workspace_bytes(const Geo& g) {
 bool backward_supported(const Geo& g) {
     // 32-bit buffer offsets: the volume rows one wave reads (16 + 2r + 1 row slabs) and one fp64
     // image must stay below 2 GiB
+    if (!plan_bwd(g).ok) return false;
     const double slab = (double)g.WO * (double)g.DO * 4.0;
     return slab * (TRB + 2 * g.r + 1) < 2147483648.0 && (double)g.H * (double)g.W * 8.0 < 2147483648.0;
 }

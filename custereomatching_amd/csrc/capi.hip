@@ -40,8 +40,10 @@ size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 int make_geo(int64_t H, int64_t W, int32_t k, int32_t layout, int32_t D, Geo* g) {
     if (H < 0 || W < 0) return fail(CUSTMA_E_ARG, "image size must be non-negative, got H=%lld W=%lld",
                                     (long long)H, (long long)W);
-    if (k < 1 || (k & 1) == 0 || k > CUSTMA_MAX_KERNEL)
-        return fail(CUSTMA_E_ARG, "kernel_size must be odd and in [1, %d], got %d", CUSTMA_MAX_KERNEL, k);
+    // even k: taps at offsets -k/2 .. k-1-k/2 (the reference's `kernel_size / 2` origin,
+    // stereo_matching_kernel.cu:44,60); r = k/2 is that origin everywhere below
+    if (k < 1 || k > CUSTMA_MAX_KERNEL)
+        return fail(CUSTMA_E_ARG, "kernel_size must be in [1, %d], got %d", CUSTMA_MAX_KERNEL, k);
     if (layout != CUSTMA_LAYOUT_FULL && layout != CUSTMA_LAYOUT_WINDOW)
         return fail(CUSTMA_E_ARG, "unknown layout %d", layout);
     if (layout == CUSTMA_LAYOUT_WINDOW && (D < 0 || (int64_t)D >= W))
@@ -128,6 +130,11 @@ void prof_end(int slot, hipStream_t s) {
     ++g_prof.n[slot];
 }
 
+// backward workspace: the fused sweep for the instantiated odd sizes, the generic path otherwise
+size_t bwd_bytes(const Geo& g) {
+    return fast_supported(g.k) ? backward_workspace_bytes(g) : backward_generic_workspace_bytes(g);
+}
+
 bool fast_supported(int k) {
     switch (k) {
 #define CUSTMA_K(KK) case KK:
@@ -190,7 +197,7 @@ size_t custma_workspace_bytes(int64_t H, int64_t W, int32_t kernel_size, int32_t
     if (make_geo(H, W, kernel_size, layout, D, &g)) return 0;
     size_t n = stats_bytes(g);
     if (op == CUSTMA_OP_DISPARITY) n += align256(disparity_partial_bytes(g));
-    if (op == CUSTMA_OP_BACKWARD || op == CUSTMA_OP_BACKWARD_RECOMPUTE) n += align256(backward_workspace_bytes(g));
+    if (op == CUSTMA_OP_BACKWARD || op == CUSTMA_OP_BACKWARD_RECOMPUTE) n += align256(bwd_bytes(g));
     if (op == CUSTMA_OP_BACKWARD_RECOMPUTE) n += align256(volume_bytes(g));
     return n;
 }
@@ -236,10 +243,10 @@ int custma_backward_band(const float* grad, const float* cost_volume, const void
     Geo g;
     int rc = make_geo(H, W, kernel_size, layout, D, &g);
     if (rc || (rc = check_dtype(dtype)) || (rc = set_band(&g, row_begin, row_end))) return rc;
-    if (!fast_supported(g.k))
-        return fail(CUSTMA_E_UNSUPPORTED, "backward supports odd kernel_size <= 15, got %d", g.k);
-    if (!backward_supported(g))
-        return fail(CUSTMA_E_UNSUPPORTED, "backward: a volume row (W_out x D_out floats) must stay below 2 GiB");
+    const bool fused = fast_supported(g.k);  // else the generic fp64 path (bwd_generic.hip)
+    if (fused && !backward_supported(g))
+        return fail(CUSTMA_E_UNSUPPORTED,
+                    "backward: a volume row (W_out x D_out floats) must stay below 2 GiB (or host planning failed)");
     if (g.H == 0 || g.W == 0 || (!camera_grad && !projector_grad)) return CUSTMA_OK;
     hipStream_t s = (hipStream_t)stream;
     if (g.HV() == 0) {  // no volume rows: gradients are zero
@@ -249,18 +256,22 @@ int custma_backward_band(const float* grad, const float* cost_volume, const void
         return rc;
     }
     if (!grad || !camera || !projector || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
-    const size_t need = stats_bytes(g) + align256(backward_workspace_bytes(g)) +
-                        (cost_volume ? 0 : align256(volume_bytes(g)));
+    const size_t need = stats_bytes(g) + align256(bwd_bytes(g)) + (cost_volume ? 0 : align256(volume_bytes(g)));
     if (workspace_bytes < need) return fail(CUSTMA_E_WORKSPACE, "workspace too small (%zu < %zu)", workspace_bytes, need);
     Stats sc, sp;
     if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
     char* ws2 = (char*)workspace + stats_bytes(g);
-    if (!cost_volume) {  // recompute the forward (fast path) into the workspace
-        float* vol = (float*)(ws2 + align256(backward_workspace_bytes(g)));
-        if ((rc = check_hip(launch_fwd_fast(camera, projector, dtype, g, sc, sp, vol, s), "backward(recompute)")))
-            return rc;
+    if (!cost_volume) {  // recompute the forward into the workspace
+        float* vol = (float*)(ws2 + align256(bwd_bytes(g)));
+        const hipError_t e = fused ? launch_fwd_fast(camera, projector, dtype, g, sc, sp, vol, s)
+                                   : launch_fwd_exact(camera, projector, dtype, g, sc, sp, vol, s);
+        if ((rc = check_hip(e, "backward(recompute)"))) return rc;
         cost_volume = vol;
     }
+    if (!fused)
+        return check_hip(launch_backward_generic(grad, cost_volume, camera, projector, dtype, g, sc, sp, camera_grad,
+                                                 projector_grad, ws2, s),
+                         "backward(generic)");
     return check_hip(launch_backward(grad, cost_volume, camera, projector, dtype, g, sc, sp, camera_grad,
                                      projector_grad, ws2, s),
                      "backward");

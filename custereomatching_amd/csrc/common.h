@@ -222,6 +222,14 @@ __device__ __forceinline__ void st_buf(float v, __amdgpu_buffer_rsrc_t r, uint32
 
 }  // namespace custma
 
+// Dynamic LDS above 64 KiB (up to the CU's 160 KiB) must be opted into per kernel.
+template <typename F>
+inline hipError_t allow_lds(F* kernel, size_t bytes) {
+    if (bytes <= 65536) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes);
+}
+
 // ---- internal launchers (one translation unit each), called from capi.hip ----
 namespace custma {
 hipError_t launch_u8_to_unit(const uint8_t* src, int64_t npix, int C, int ch, int out_dtype, void* out,
@@ -237,6 +245,11 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
                             int64_t* idx, float* best, int32_t* n_rechecked, void* ws, hipStream_t s);
 size_t backward_workspace_bytes(const Geo& g);
 bool backward_supported(const Geo& g);
+// generic backward (any k; bwd_generic.hip)
+size_t backward_generic_workspace_bytes(const Geo& g);
+hipError_t launch_backward_generic(const float* grad, const float* vol, const void* cam, const void* proj, int dtype,
+                                   const Geo& g, Stats sc, Stats sp, float* dcam, float* dproj, void* ws,
+                                   hipStream_t s);
 hipError_t launch_backward(const float* grad, const float* vol, const void* cam, const void* proj, int dtype,
                            const Geo& g, Stats sc, Stats sp, float* dcam, float* dproj, void* ws, hipStream_t s);
 bool fast_supported(int k);

@@ -141,6 +141,8 @@ hipError_t launch_fwd_exact(const void* cam, const void* proj, int dtype, const 
     const int nDC = (int)(g.layout == CUSTMA_LAYOUT_WINDOW ? cdiv(TWX + g.D, TDX) : cdiv(g.W, TDX));
     const int64_t blocks = g.HV() * nWT * nDC;
     const size_t lds = sizeof(float) * (g.k * (TWX + 2 * g.r) + g.k * (TDX + 2 * g.r) + 2 * TWX + 2 * TDX);
+    hipError_t e = dtype == CUSTMA_F16 ? allow_lds(k_fwd_exact<__half>, lds) : allow_lds(k_fwd_exact<float>, lds);
+    if (e != hipSuccess) return e;
     if (dtype == CUSTMA_F16)
         hipLaunchKernelGGL(k_fwd_exact<__half>, dim3((unsigned)blocks), dim3(256), lds, s, (const __half*)cam,
                            (const __half*)proj, g, sc, sp, out, nWT, nDC);

@@ -141,14 +141,18 @@ hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo&
     const dim3 grid((unsigned)cdiv(g.W, TX), (unsigned)cdiv(g.H, TY), 2);
     const int LX = TX + 2 * g.r, LY = TY + 2 * g.r;
     const size_t lds = sizeof(double) * 2 * LY * TX + sizeof(float) * LY * LX;
+    hipError_t err = hipSuccess;
     auto go = [&](auto kc) {
         constexpr int KT = decltype(kc)::value;
-        if (dtype == CUSTMA_F16)
+        if (dtype == CUSTMA_F16) {
+            if ((err = allow_lds(k_stats<__half, KT>, lds)) != hipSuccess) return;
             hipLaunchKernelGGL((k_stats<__half, KT>), grid, dim3(256), lds, s, (const __half*)cam, (const __half*)proj,
                                g, sc, sp);
-        else
+        } else {
+            if ((err = allow_lds(k_stats<float, KT>, lds)) != hipSuccess) return;
             hipLaunchKernelGGL((k_stats<float, KT>), grid, dim3(256), lds, s, (const float*)cam, (const float*)proj, g,
                                sc, sp);
+        }
     };
     switch (g.k) {
 #define CUSTMA_K(KK) \
@@ -157,7 +161,7 @@ hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo&
 #undef CUSTMA_K
         default: go(std::integral_constant<int, 0>{});
     }
-    return hipGetLastError();
+    return err != hipSuccess ? err : hipGetLastError();
 }
 
 }  // namespace custma

@@ -1,9 +1,10 @@
 """Row-band sharding of one image pair across GPUs.
 
-Output row h of the cost volume reads only image rows h-r .. h+r (r = k//2,
-custma/src/stereo_matching_kernel.cu:44,60), so the path shards by row band
-with no data-path collective: rank g owns rows [b_g, e_g) of both images
-and of the volume, and needs r halo rows from each neighbour.
+Output row h of the cost volume reads only image rows h-o .. h+a (o = k//2,
+a = k-1-o; o = a = r for odd k; custma/src/stereo_matching_kernel.cu:44,60),
+so the path shards by row band with no data-path collective: rank g owns rows
+[b_g, e_g) of both images and of the volume, and needs o halo rows from the
+rank above and a from the rank below.
 
 * forward: one neighbour exchange of r x W pixels per image per side
   (``torch.distributed.batch_isend_irecv`` -- RCCL point-to-point over xGMI
@@ -23,6 +24,7 @@ Tests on CPU (gloo) inject the oracle as the backend; the product never does.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -57,39 +59,62 @@ class HipBackend:
 
 
 class RowBandGroup:
-    """Rank/world/radius bookkeeping plus the two halo primitives."""
+    """Rank/world/halo bookkeeping plus the two halo primitives.
 
-    def __init__(self, kernel_size: int, group=None):
+    The halo must come from the immediate neighbour, so every band needs at
+    least max(o, a) rows.  That is checked for ALL ranks before any
+    point-to-point call, so every rank raises together instead of the thin
+    ranks raising while their neighbours wait in ``batch_isend_irecv``: from
+    ``H`` (the global height, bands = ``band_bounds``) without communication,
+    or else with one MIN all-reduce of the band heights."""
+
+    def __init__(self, kernel_size: int, group=None, n: Optional[int] = None, H: Optional[int] = None,
+                 device=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.r = kernel_size // 2
+        self.o = kernel_size // 2
+        self.a = kernel_size - 1 - self.o
+        need = max(self.o, self.a)
+        if self.world > 1 and need > 0:
+            if H is not None:
+                thinnest = min(e - b for b, e in (band_bounds(H, self.world, q) for q in range(self.world)))
+            elif n is not None:
+                t = torch.tensor([int(n)], dtype=torch.int64, device=device)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+                thinnest = int(t.item())
+            else:
+                thinnest = None
+            if thinnest is not None and thinnest < need:
+                raise ValueError(f"the thinnest row band has {thinnest} rows, fewer than the {need} halo rows "
+                                 f"kernel_size {kernel_size} needs from a neighbour")
 
     def _peer(self, rank):
         return dist.get_global_rank(self.group, rank) if self.group is not None else rank
 
     def halo_sizes(self) -> Tuple[int, int]:
-        top = self.r if self.rank > 0 else 0
-        bot = self.r if self.rank < self.world - 1 else 0
+        """Rows received from the rank above (o) and from the rank below (a)."""
+        top = self.o if self.rank > 0 else 0
+        bot = self.a if self.rank < self.world - 1 else 0
         return top, bot
 
     def exchange_halo(self, band: torch.Tensor) -> torch.Tensor:
         """[n, W] owned rows -> [top + n + bot, W] with the neighbours' edge rows."""
-        r = self.r
         top, bot = self.halo_sizes()
         if top == 0 and bot == 0:
             return band
         n = band.shape[0]
-        if n < r:
-            raise ValueError(f"row band of {n} rows is thinner than the halo radius {r}")
+        if n < max(self.o, self.a):
+            raise ValueError(f"row band of {n} rows is thinner than the halo ({self.o} / {self.a} rows)")
         out = torch.empty((top + n + bot,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
         out[top:top + n].copy_(band)
         ops = []
+        # the rank above needs my first a rows (its bottom halo); the rank below my last o rows
         if top:
-            ops.append(dist.P2POp(dist.isend, band[:r].contiguous(), self._peer(self.rank - 1), self.group))
+            ops.append(dist.P2POp(dist.isend, band[:self.a].contiguous(), self._peer(self.rank - 1), self.group))
             ops.append(dist.P2POp(dist.irecv, out[:top], self._peer(self.rank - 1), self.group))
         if bot:
-            ops.append(dist.P2POp(dist.isend, band[n - r:].contiguous(), self._peer(self.rank + 1), self.group))
+            ops.append(dist.P2POp(dist.isend, band[n - self.o:].contiguous(), self._peer(self.rank + 1), self.group))
             ops.append(dist.P2POp(dist.irecv, out[top + n:], self._peer(self.rank + 1), self.group))
         for req in dist.batch_isend_irecv(ops):
             req.wait()
@@ -99,15 +124,15 @@ class RowBandGroup:
         """[top + n + bot, W] partial gradients -> [n, W] owned rows with the
         neighbours' halo partials added (each neighbour sends the partials of
         rows this rank owns)."""
-        r = self.r
         top, bot = self.halo_sizes()
         own = buf[top:top + n]
         if top == 0 and bot == 0:
             return own.contiguous()
         own = own.clone()
         ops = []
-        from_up = torch.empty((r,) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device) if top else None
-        from_dn = torch.empty((r,) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device) if bot else None
+        # partials of my first a rows come from the rank above, of my last o rows from the rank below
+        from_up = torch.empty((self.a,) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device) if top else None
+        from_dn = torch.empty((self.o,) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device) if bot else None
         if top:
             ops.append(dist.P2POp(dist.isend, buf[:top].contiguous(), self._peer(self.rank - 1), self.group))
             ops.append(dist.P2POp(dist.irecv, from_up, self._peer(self.rank - 1), self.group))
@@ -116,10 +141,10 @@ class RowBandGroup:
             ops.append(dist.P2POp(dist.irecv, from_dn, self._peer(self.rank + 1), self.group))
         for req in dist.batch_isend_irecv(ops):
             req.wait()
-        if top:
-            own[:r] += from_up
-        if bot:
-            own[n - r:] += from_dn
+        if top and self.a:
+            own[:self.a] += from_up
+        if bot and self.o:
+            own[n - self.o:] += from_dn
         return own
 
 
@@ -131,13 +156,18 @@ class _RowBandStereoMatching(torch.autograd.Function):
         top, _ = rbg.halo_sizes()
         n = cam_band.shape[0]
         vol = backend.forward(ch, ph, D, kernel_size, layout, precision, (top, top + n))
-        ctx.save_for_backward(ch, ph, vol)
+        # the haloed images are saved; the returned volume only weakly (see _StereoMatching)
+        ctx.save_for_backward(ch, ph)
+        ctx.vol_ref = weakref.ref(vol)
+        ctx.vol_version = vol._version
         ctx.meta = (D, kernel_size, layout, rbg, backend, top, n)
         return vol
 
     @staticmethod
     def backward(ctx, grad):
-        ch, ph, vol = ctx.saved_tensors
+        ch, ph = ctx.saved_tensors
+        vol = ctx.vol_ref()
+        vol = vol.detach() if vol is not None and vol._version == ctx.vol_version else None
         D, k, layout, rbg, backend, top, n = ctx.meta
         want_c, want_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         gc, gp = backend.backward(grad.contiguous(), ch, ph, D, k, layout, (top, top + n), want_c, want_p, vol)
@@ -148,18 +178,20 @@ class _RowBandStereoMatching(torch.autograd.Function):
 
 def stereo_matching_rowband(cam_band: torch.Tensor, proj_band: torch.Tensor, D: int, kernel_size: int,
                             layout: str = "full", precision: Optional[str] = None, group=None,
-                            backend=None) -> torch.Tensor:
+                            backend=None, H: Optional[int] = None) -> torch.Tensor:
     """Distributed ``stereo_matching``: every rank passes its own row band of
     both images (rows ``band_bounds(H, world, rank)``) and gets the matching
-    rows of the cost volume; ``backward`` yields gradients of its own rows."""
-    rbg = RowBandGroup(kernel_size, group)
+    rows of the cost volume; ``backward`` yields gradients of its own rows.
+    ``H`` (the global height) lets the band-thickness check skip its all-reduce."""
+    rbg = RowBandGroup(kernel_size, group, n=cam_band.shape[0], H=H, device=cam_band.device)
     return _RowBandStereoMatching.apply(cam_band, proj_band, D, kernel_size, layout, precision, rbg,
                                         backend or HipBackend())
 
 
-def stereo_disparity_rowband(cam_band, proj_band, D, kernel_size, layout="full", group=None, backend=None):
+def stereo_disparity_rowband(cam_band, proj_band, D, kernel_size, layout="full", group=None, backend=None,
+                             H: Optional[int] = None):
     """Distributed fused disparity for the owned rows (halo exchange only)."""
-    rbg = RowBandGroup(kernel_size, group)
+    rbg = RowBandGroup(kernel_size, group, n=cam_band.shape[0], H=H, device=cam_band.device)
     ch = rbg.exchange_halo(cam_band.contiguous())
     ph = rbg.exchange_halo(proj_band.contiguous())
     top, _ = rbg.halo_sizes()

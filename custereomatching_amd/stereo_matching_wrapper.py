@@ -30,6 +30,7 @@ scalar type Float but found ..."`` like ``data_ptr<float>()`` does.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -181,13 +182,22 @@ def cost_volume_backward(cost_volume_grad: torch.Tensor, camera: torch.Tensor, p
 
 
 class _StereoMatching(torch.autograd.Function):
-    """Reference: custma/stereo_matching_wrapper.py:7-33."""
+    """Reference: custma/stereo_matching_wrapper.py:7-33.
+
+    Saves only the two images, as the reference does (:16).  The backward also
+    needs the forward's costs (V = g * cost / S); it reads the returned volume
+    when that tensor is still alive and unmodified (a weak reference plus its
+    version counter -- no reference cycle, no extra lifetime), and otherwise
+    recomputes the volume inside the backward call (CUSTMA_OP_BACKWARD_RECOMPUTE).
+    So an in-place edit of the returned volume, or dropping it before
+    ``.backward()``, behaves as with the reference."""
 
     @staticmethod
     def forward(ctx, camera_image, projector_image, D, kernel_size, layout="full", precision=None):
         vol = cost_volume_forward(camera_image, projector_image, D, kernel_size, layout, precision)
-        # the backward reads the returned volume (V = g * cost / S); saved like any output
-        ctx.save_for_backward(camera_image, projector_image, vol)
+        ctx.save_for_backward(camera_image, projector_image)
+        ctx.vol_ref = weakref.ref(vol)
+        ctx.vol_version = vol._version
         ctx.D = D
         ctx.kernel_size = kernel_size
         ctx.layout = layout
@@ -195,7 +205,12 @@ class _StereoMatching(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, cost_volume_grad):
-        camera_image, projector_image, vol = ctx.saved_tensors
+        camera_image, projector_image = ctx.saved_tensors
+        vol = ctx.vol_ref()
+        if vol is not None and vol._version != ctx.vol_version:
+            vol = None  # edited in place after the forward: recompute the costs
+        if vol is not None:
+            vol = vol.detach()
         want_c, want_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         gc, gp = cost_volume_backward(cost_volume_grad.contiguous(), camera_image, projector_image,
                                       ctx.kernel_size, ctx.layout, ctx.D, camera_grad=want_c,

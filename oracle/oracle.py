@@ -144,6 +144,13 @@ def cost_error_bound(k: int) -> float:
     return (k * k + 6) * u
 
 
+def fast_tolerance(k: int) -> float:
+    """The gate every fast-path cost is held to: BASELINE north_star's 1e-5 on the
+    float cost volume, or the tighter worst-case bound where that is below it
+    (k <= 11)."""
+    return min(1e-5, cost_error_bound(k))
+
+
 def image_u8_to_unit(image, channel=0, dtype=np.float32):
     """The reference driver's preprocessing (examples/verify.py:138-142, 148):
     ``np.array(cv2.imread(...)) / 255`` (numpy float64 true division), then

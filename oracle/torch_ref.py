@@ -19,9 +19,14 @@ EPS = 1e-8  # examples/verify.py:112
 
 
 def patches(img: torch.Tensor, k: int) -> torch.Tensor:
-    """[H, W] -> [H, W, k*k] zero-padded patches, tap order (i, j) row-major."""
-    r = k // 2
-    x = F.pad(img[None, None], (r, r, r, r), mode="constant", value=0.0)
+    """[H, W] -> [H, W, k*k] zero-padded patches, tap order (i, j) row-major.
+
+    Taps sit at offsets -k//2 .. k-1-k//2 (stereo_matching_kernel.cu:44,60); for
+    odd k that is verify.py:26's symmetric pad, for even k the reference's CUDA
+    kernel (verify.py's symmetric pad would give H+1 patches there)."""
+    o = k // 2
+    a = k - 1 - o
+    x = F.pad(img[None, None], (o, a, o, a), mode="constant", value=0.0)
     x = x.unfold(3, k, 1).unfold(2, k, 1).permute(0, 1, 2, 3, 5, 4)  # [1,1,H,W,k,k]
     H, W = img.shape
     return x.reshape(H, W, k * k)
@@ -46,7 +51,7 @@ def forward_backward(cam, proj, k, grad=None, proj_grad=True, row_chunk=None):
     returned (None) and gradients are accumulated band by band.
     """
     H, W = cam.shape
-    r = k // 2
+    o, a_ = k // 2, k - 1 - k // 2  # halo rows above / below a band
     if row_chunk is None or row_chunk >= H:
         c = cam.detach().clone().requires_grad_(True)
         p = proj.detach().clone().requires_grad_(proj_grad)
@@ -57,7 +62,7 @@ def forward_backward(cam, proj, k, grad=None, proj_grad=True, row_chunk=None):
     gp = torch.zeros_like(proj)
     for h0 in range(0, H, row_chunk):
         h1 = min(H, h0 + row_chunk)
-        a0, a1 = max(0, h0 - r), min(H, h1 + r)
+        a0, a1 = max(0, h0 - o), min(H, h1 + a_)
         c = cam[a0:a1].detach().clone().requires_grad_(True)
         p = proj[a0:a1].detach().clone().requires_grad_(proj_grad)
         # The band's own zero padding differs from the image's at interior
@@ -86,10 +91,10 @@ def forward_only(cam, proj, k, row_chunk=None):
         if row_chunk is None or row_chunk >= cam.shape[0]:
             return cost_volume(cam, proj, k)
         H = cam.shape[0]
-        r = k // 2
+        o, a_ = k // 2, k - 1 - k // 2
         outs = []
         for h0 in range(0, H, row_chunk):
             h1 = min(H, h0 + row_chunk)
-            a0, a1 = max(0, h0 - r), min(H, h1 + r)
+            a0, a1 = max(0, h0 - o), min(H, h1 + a_)
             outs.append(cost_volume(cam[a0:a1], proj[a0:a1], k)[h0 - a0:h1 - a0])
         return torch.cat(outs)

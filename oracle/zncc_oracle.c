@@ -66,7 +66,7 @@ int orc_volume_dims(int64_t H, int64_t W, int layout, int D, int64_t* WO, int64_
  * exactly this sequence for its camera pixel (h,w) and projector pixel (h,d),
  * so hoisting it per pixel is bit-identical. */
 int orc_stats(const float* img, int64_t H, int64_t W, int k, int contract, float* mean, float* sq) {
-    if (k <= 0 || (k & 1) == 0) return -3;
+    if (k <= 0) return -3; /* even k: taps at offsets -k/2 .. k-1-k/2, as .cu:44,60 */
     const int64_t r = k / 2;
     for (int64_t h = 0; h < H; ++h)
         for (int64_t w = 0; w < W; ++w) {
@@ -94,7 +94,7 @@ int orc_forward_literal(const float* cam, const float* proj, int64_t H, int64_t 
     int64_t WO, DO;
     int rc = orc_volume_dims(H, W, layout, D, &WO, &DO);
     if (rc) return rc;
-    if (k <= 0 || (k & 1) == 0) return -3;
+    if (k <= 0) return -3; /* even k: taps at offsets -k/2 .. k-1-k/2, as .cu:44,60 */
     const int64_t r = k / 2;
     for (int64_t h = 0; h < H; ++h)
         for (int64_t w = 0; w < WO; ++w)
@@ -131,7 +131,7 @@ int orc_forward(const float* cam, const float* proj, int64_t H, int64_t W, int k
     int64_t WO, DO;
     int rc = orc_volume_dims(H, W, layout, D, &WO, &DO);
     if (rc) return rc;
-    if (k <= 0 || (k & 1) == 0) return -3;
+    if (k <= 0) return -3; /* even k: taps at offsets -k/2 .. k-1-k/2, as .cu:44,60 */
     const int64_t r = k / 2, K = (int64_t)k * k;
     float* cm = (float*)malloc(sizeof(float) * H * W);
     float* cx = (float*)malloc(sizeof(float) * H * W);
@@ -174,7 +174,7 @@ int orc_forward_f64(const float* cam, const float* proj, int64_t H, int64_t W, i
     int64_t WO, DO;
     int rc = orc_volume_dims(H, W, layout, D, &WO, &DO);
     if (rc) return rc;
-    if (k <= 0 || (k & 1) == 0) return -3;
+    if (k <= 0) return -3; /* even k: taps at offsets -k/2 .. k-1-k/2, as .cu:44,60 */
     const int64_t r = k / 2, K = (int64_t)k * k;
     double* xt = (double*)malloc(sizeof(double) * W * K);
     double* yt = (double*)malloc(sizeof(double) * W * K);
@@ -228,7 +228,7 @@ int orc_backward(const float* g, const float* cam, const float* proj, int64_t H,
     int64_t WO, DO;
     int rc = orc_volume_dims(H, W, layout, D, &WO, &DO);
     if (rc) return rc;
-    if (k <= 0 || (k & 1) == 0) return -3;
+    if (k <= 0) return -3; /* even k: taps at offsets -k/2 .. k-1-k/2, as .cu:44,60 */
     const int64_t r = k / 2, K = (int64_t)k * k;
     float* cm = (float*)malloc(sizeof(float) * H * W);
     float* cx = (float*)malloc(sizeof(float) * H * W);
@@ -302,7 +302,7 @@ int orc_backward_f64(const float* g, const float* cam, const float* proj, int64_
     int64_t WO, DO;
     int rc = orc_volume_dims(H, W, layout, D, &WO, &DO);
     if (rc) return rc;
-    if (k <= 0 || (k & 1) == 0) return -3;
+    if (k <= 0) return -3; /* even k: taps at offsets -k/2 .. k-1-k/2, as .cu:44,60 */
     const int64_t r = k / 2, K = (int64_t)k * k;
     double* xt = (double*)malloc(sizeof(double) * W * K);
     double* yt = (double*)malloc(sizeof(double) * W * K);

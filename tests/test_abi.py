@@ -49,10 +49,12 @@ def test_abi_version_and_dims():
     with pytest.raises(ValueError):
         _lib.volume_dims(128, 256, _lib.LAYOUT_WINDOW, 256)
     assert _lib.workspace_bytes(64, 64, 5, 0, 0, _lib.OP_FORWARD) > 0
-    assert _lib.workspace_bytes(64, 64, 4, 0, 0, _lib.OP_FORWARD) == 0  # even kernel rejected
+    assert _lib.workspace_bytes(64, 64, 4, 0, 0, _lib.OP_FORWARD) > 0  # even k: the reference's k/2 origin
+    assert _lib.workspace_bytes(64, 64, 63, 0, 0, _lib.OP_BACKWARD) > 0  # generic backward
+    assert _lib.workspace_bytes(64, 64, 64, 0, 0, _lib.OP_FORWARD) == 0  # above CUSTMA_MAX_KERNEL
 
 
-@pytest.mark.parametrize("k", [0, 2, 33, -1])
+@pytest.mark.parametrize("k", [0, 64, 99, -1])
 def test_forward_rejects_bad_kernel_without_device(k):
     from custereomatching_amd import _lib
 
@@ -70,7 +72,9 @@ def test_entry_points_validate_before_launch():
     assert L.custma_forward(None, None, 0, 8, 8, 5, 1, 8, 1, None, None, 0, None) == _lib.E_ARG  # D >= W
     assert L.custma_forward(None, None, 0, 8, 8, 5, 0, 0, 1, None, None, 0, None) == _lib.E_NULL
     assert L.custma_forward(None, None, 0, 0, 8, 5, 0, 0, 1, None, None, 0, None) == 0  # empty image: no-op
-    assert L.custma_backward(None, None, None, None, 0, 8, 8, 17, 0, 0, None, None, None, 0, None) == _lib.E_UNSUPPORTED
+    # k = 17 has no fused instantiation: the generic backward takes it, validating first
+    fake = 4096  # never dereferenced: the null gradient is rejected before any launch
+    assert L.custma_backward(None, None, None, None, 0, 8, 8, 17, 0, 0, fake, None, None, 0, None) == _lib.E_NULL
     assert L.custma_argmax(None, 4, 0, None, None, None) == _lib.E_ARG
     assert L.custma_disparity(None, None, 0, 8, 8, 5, 0, 0, None, None, None, None, 0, None) == _lib.E_NULL
 

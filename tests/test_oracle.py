@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from tests.golden.inputs import make_pair
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 SMALL = sorted(p for p in glob.glob(os.path.join(GOLD, "*.npz")) if not os.path.basename(p).startswith("verify_"))
@@ -124,3 +125,42 @@ def test_argmax_first_index_on_ties():
     v = np.array([[1, 3, 3, 2], [0, 0, 0, 0]], np.float32)
     idx, best = O.argmax(v)
     assert idx.tolist() == [1, 0] and best.tolist() == [3, 0]
+
+
+# ---- the timed CPU baseline (oracle/torch_ref.py) pinned to the reference's torch path ----
+
+@pytest.mark.parametrize("name", ["tiny_16x24_k5", "tex_20x48_k9", "quant_24x48_k5", "tall_40x12_k11",
+                                  "row_1x32_k5"])
+@pytest.mark.parametrize("row_chunk", [None, 7])
+def test_torch_ref_matches_reference_torch_goldens(name, row_chunk):
+    """bench.py's cpu_baseline runs oracle/torch_ref.py: it must be the reference's
+    examples/verify.py:81-133 computation (goldens made by importing it), whole and in
+    haloed row bands (row_chunk)."""
+    import torch
+
+    from oracle import torch_ref as T
+
+    z = np.load(os.path.join(GOLD, f"{name}.npz"))
+    cam, proj, k = torch.from_numpy(z["cam"]), torch.from_numpy(z["proj"]), int(z["k"])
+    vol, gc, gp = T.forward_backward(cam, proj, k, row_chunk=row_chunk)
+    if vol is None:
+        vol = T.forward_only(cam, proj, k, row_chunk=row_chunk)
+    assert np.abs(vol.numpy() - z["vol32"]).max() <= 2e-6
+    for got, ref in ((gc, z["cg64"]), (gp, z["pg64"])):
+        assert np.abs(got.numpy() - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("k", [2, 4, 6])
+def test_torch_ref_even_k_matches_c_oracle(k):
+    """Even k (taps at -k/2 .. k/2-1, stereo_matching_kernel.cu:44,60): the torch
+    restatement and the C oracle agree in fp64."""
+    import torch
+
+    from oracle import torch_ref as T
+
+    cam, proj = make_pair(13, 17, 4, seed=k)
+    v, gc, gp = T.forward_backward(torch.from_numpy(cam).double(), torch.from_numpy(proj).double(), k)
+    rc, rp = O.backward_f64(np.ones((13, 17, 17), np.float32), cam, proj, k)
+    assert np.abs(v.numpy() - O.forward_f64(cam, proj, k)).max() <= 1e-9
+    assert np.abs(gc.numpy() - rc).max() <= 1e-9 * max(1.0, np.abs(rc).max())
+    assert np.abs(gp.numpy() - rp).max() <= 1e-9 * max(1.0, np.abs(rp).max())

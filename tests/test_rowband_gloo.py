@@ -48,7 +48,7 @@ class OracleBackend:
         return torch.from_numpy(idx), torch.from_numpy(best)
 
 
-def _worker(rank, world, port, H, W, k, D, layout, q):
+def _worker(rank, world, port, H, W, k, D, layout, q, pass_h=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,7 +60,11 @@ def _worker(rank, world, port, H, W, k, D, layout, q):
         c = torch.from_numpy(cam[b:e].copy()).requires_grad_(True)
         p = torch.from_numpy(proj[b:e].copy()).requires_grad_(True)
         be = OracleBackend()
-        vol = stereo_matching_rowband(c, p, D, k, layout, backend=be)
+        try:
+            vol = stereo_matching_rowband(c, p, D, k, layout, backend=be, H=H if pass_h else None)
+        except ValueError as ex:  # band thinner than the halo: every rank must raise
+            q.put((rank, "ValueError", str(ex)))
+            return
         lay, Dl = OracleBackend._lay(layout, D)
         g = np.random.default_rng(5).standard_normal(O.volume_shape(H, W, lay, Dl)).astype(np.float32)
         vol.backward(torch.from_numpy(g[b:e].copy()))
@@ -70,19 +74,26 @@ def _worker(rank, world, port, H, W, k, D, layout, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,layout", [(2, "full"), (3, "window"), (2, "window")])
-def test_rowband_matches_single_device(world, layout):
-    H, W, k, D = 23, 28, 5, 6
+def _run(world, H, W, k, D, layout, pass_h=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, k, D, layout, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, k, D, layout, q, pass_h)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=240) for _ in range(world)])
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,layout,k", [(2, "full", 5), (3, "window", 5), (2, "window", 5), (2, "full", 4),
+                                            (3, "window", 6)])
+def test_rowband_matches_single_device(world, layout, k):
+    """Odd k: r halo rows each side; even k: k/2 rows from the rank above, k/2-1 from below."""
+    H, W, D = 23, 28, 6
+    res = _run(world, H, W, k, D, layout)
     cam, proj = make_pair(H, W, max(D, 1), seed=17)
     lay, Dl = OracleBackend._lay(layout, D)
     vol = O.forward(cam, proj, k, layout=lay, D=Dl)
@@ -97,6 +108,14 @@ def test_rowband_matches_single_device(world, layout):
         assert np.array_equal(idx, ridx[b:e])
         covered += e - b
     assert covered == H
+
+
+@pytest.mark.parametrize("pass_h", [False, True])
+def test_rowband_thin_band_raises_on_every_rank(pass_h):
+    """H = 9 over 2 ranks at k = 11 (bands 5 and 4 < r = 5): every rank raises
+    before any halo exchange (no rank left waiting in batch_isend_irecv)."""
+    res = _run(2, 9, 16, 11, 2, "full", pass_h)
+    assert [t[1] for t in res] == ["ValueError", "ValueError"]
 
 
 def test_band_bounds_partition():
