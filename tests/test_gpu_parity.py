@@ -81,7 +81,9 @@ def test_fast_forward_within_bound(gpu, case, layout):
     assert got.shape == ref.shape
     assert np.abs(got - ref).max() <= O.fast_tolerance(k)
     truth = O.forward_f64(cam, proj, k, layout=lay, D=Dl)
-    assert np.abs(got - truth).max() <= O.fast_tolerance(k)
+    # vs the fp64 truth: the reference's own worst-case rounding (k > 15 runs the exact
+    # reference arithmetic, whose k^2-long fp32 chain can exceed 1e-5 of the truth)
+    assert np.abs(got - truth).max() <= O.cost_error_bound(k)
 
 
 REM_CASES = [
