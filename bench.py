@@ -2,43 +2,65 @@
 """Benchmark: ZNCC stereo cost volume, forward + backward (grad wrt both images).
 
 BASELINE.json metric: "cost-volume Mvoxels/s (H x W x D) fwd+bwd at 1/2/4/8
-MI355X; % HBM roofline".  Workload = BASELINE configs[2]: 1024 x 1024 fp32
-image pair per GPU, D = 128, window 9, forward + backward with gradients
-w.r.t. both images.  Layout "full" is what the reference op returns
-([H, W, W]; D ignored, custma/src/stereo_matching_kernel.cu:14,200), so a
-voxel is one element of that volume (1.07e9 per step per GPU).
+MI355X; % HBM roofline".  One step = forward (volume written to HBM) +
+backward (synthetic upstream gradient read from HBM, both image gradients
+written) through the drop-in autograd op; a voxel is one element of the
+returned volume.  Workloads (--workload):
 
-One step = forward (volume written to HBM) + backward (synthetic upstream
-gradient read from HBM, both image gradients written), through the drop-in
-autograd op.  N > 1 GPUs (launched by torch.distributed.run): weak scaling by
-row bands -- each rank owns a 1024-row band of a (1024 N)-row image pair and
-exchanges k//2 halo rows with its neighbours over RCCL (custereomatching_amd.
-rowband); no other collective on the data path.
+  c5 (default)  BASELINE configs[4]: 4096 x 8192 fp16 pair, D = 256, k = 11,
+                window layout [H, W-D, D+1] (8.35e9 voxels per step).  STRONG
+                scaling: N ranks split the rows (custereomatching_amd.rowband,
+                band_bounds), exchanging k//2 halo rows with their neighbours over
+                RCCL (torch.distributed "nccl"); no other collective on the data path.
+  c2            BASELINE configs[2]: 1024 x 1024 fp32, D = 128, k = 9, the reference's
+                full [H, W, W] volume; WEAK scaling, one 1024-row band per GPU.
+
+`python bench.py --gpus N` with N > 1 and no launcher environment starts
+`torch.distributed.run` itself (a child process, before any GPU call) and exits
+with its status; under torchrun it reads RANK / LOCAL_RANK / WORLD_SIZE.
 
 Prints ONE JSON line (rank 0).  Extra objects:
-  roofline      dominant kernel (the backward sweep, k_bwd_coop) -- algorithmic
-                bytes / its average duration from HIP events around its launches in
-                the timed region; "kernels" has the same for the forward sweep
-  cpu_baseline  the reference's torch CPU path (oracle/torch_ref.py restating
-                examples/verify.py:81-133) on a bounded row band, rank 0, N=1
+  roofline      dominant kernel of the step -- algorithmic bytes / its average
+                duration from HIP events around its launches in the timed region;
+                `traffic` = HBM bytes per launch from rocprofv3 PMC passes
+                (FETCH_SIZE, WRITE_SIZE; separate passes, gfx950 corrections) run
+                by this process on the same workload (rank 0, N = 1)
+  kernels       the same figures for the forward and backward sweeps
   north_star    BASELINE configs[3]: 2048 x 2048 fp16, D = 256, k = 11, window
-                layout forward, % of HBM roofline
+                forward, fraction of the 8 TB/s HBM roofline (N = 1)
+  config2       the c2 workload's fwd+bwd step at N = 1 (context across rounds)
+  cpu_baseline  the reference's torch CPU path (oracle/torch_ref.py restating
+                examples/verify.py:81-133) on a bounded row band of the same
+                workload, rank 0, N = 1
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    "c5": dict(H=4096, W=8192, k=11, D=256, layout="window", dtype=torch.float16, scaling="strong",
+               desc="BASELINE configs[4]: fwd+bwd (grads wrt both images), 4096x8192 fp16 pair, D=256, "
+                    "window k=11, window layout [H, W-D, D+1]; strong scaling over row bands"),
+    "c2": dict(H=1024, W=1024, k=9, D=128, layout="full", dtype=torch.float32, scaling="weak",
+               desc="BASELINE configs[2]: fwd+bwd (grads wrt both images) of the reference op's full volume, "
+                    "1024x1024 fp32 pair per GPU, D=128, window k=9; weak scaling (1024 rows per GPU)"),
+}
 
 
 def parse():
@@ -46,15 +68,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--H", type=int, default=1024, help="rows per GPU")
-    ap.add_argument("--W", type=int, default=1024)
-    ap.add_argument("--k", type=int, default=9)
-    ap.add_argument("--D", type=int, default=128)
-    ap.add_argument("--layout", default="full", choices=["full", "window"])
+    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
     ap.add_argument("--precision", default="fast", choices=["fast", "exact"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=96, help="row band timed for the CPU baseline")
+    ap.add_argument("--no-config2", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearsal of N ranks on fewer GPUs (halo staged through host memory)")
+    ap.add_argument("--pmc-child", default=None, choices=["fwd", "bwd"], help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-rows", type=int, default=None, help="rows of the CPU-baseline sample")
     return ap.parse_args()
 
 
@@ -90,35 +113,17 @@ class EventTimer:
         return sum(s.elapsed_time(e) for s, e in self.pairs) / max(1, len(self.pairs))
 
 
-def cpu_baseline(args, k):
-    """Reference torch path on CPU, bounded sample (rank 0, N = 1 only)."""
-    from oracle import torch_ref
+def fwd_kernel_name(layout, W, D):
+    """The forward sweep the library launches (sweep_wave.hip launch_fwd_fast)."""
+    if layout == "full":
+        return "k_sweep_fwd"
+    return "k_fwd_tile" if D + 1 <= 257 else "k_fwd_wave"
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
-    rows = args.cpu_rows
-    r = k // 2
-    cam, proj = synth_pair(rows + 2 * r, args.W, args.D, 1234, "cpu")
-    best = float("inf")
-    t_end = time.time() + 25.0
-    runs = 0
-    torch_ref.forward_backward(cam[: 2 * r + 8], proj[: 2 * r + 8], k)  # warm-up (allocator, threads)
-    while runs < 3 and (runs == 0 or time.time() < t_end):
-        t0 = time.perf_counter()
-        _, gc, gp = torch_ref.forward_backward(cam, proj, k, proj_grad=True)
-        best = min(best, time.perf_counter() - t0)
-        runs += 1
-    vox = (rows + 2 * r) * args.W * args.W
-    return {
-        "value": round(vox / best / 1e6, 2),
-        "unit": "Mvoxels/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": (f"torch CPU restatement of examples/verify.py:81-133 (unfold+bmm+autograd, fp32, "
-                   f"camera+projector grads) on a {rows + 2 * r}x{args.W} band, k={k}, full [H,W,W] "
-                   f"volume = {vox / 1e6:.1f} Mvox per run, best of {runs}; cpu={_cpu_model()}"),
-    }
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def _cpu_model():
@@ -129,6 +134,39 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def cpu_baseline(wl, rows):
+    """Reference torch path on CPU, bounded sample of the workload (rank 0, N = 1 only)."""
+    from oracle import torch_ref
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    k, D, W, layout = wl["k"], wl["D"], wl["W"], wl["layout"]
+    halo = k - 1
+    # fp16 workloads: the reference torch path is fp32; it runs on the fp16 images widened
+    cam, proj = synth_pair(rows + halo, W, D, 1234, "cpu", wl["dtype"])
+    cam, proj = cam.float(), proj.float()
+    torch_ref.forward_backward(cam[: halo + 2], proj[: halo + 2], k, layout=layout, D=D)  # warm-up
+    best, runs, t_end = float("inf"), 0, time.time() + 25.0
+    while runs < 3 and (runs == 0 or time.time() < t_end):
+        t0 = time.perf_counter()
+        torch_ref.forward_backward(cam, proj, k, proj_grad=True, layout=layout, D=D)
+        best = min(best, time.perf_counter() - t0)
+        runs += 1
+    WO, DO = (W, W) if layout == "full" else (W - D, D + 1)
+    vox = (rows + halo) * WO * DO
+    what = "unfold+bmm" if layout == "full" else "unfold + blocked bmm with the window's diagonals read out"
+    return {
+        "value": round(vox / best / 1e6, 2),
+        "unit": "Mvoxels/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"torch CPU restatement of examples/verify.py:81-133 ({what} + autograd, fp32, camera + "
+                   f"projector grads) on a {rows + halo}x{W} band of the workload, k={k}, {layout} volume = "
+                   f"{vox / 1e6:.1f} Mvox per run, best of {runs}; cpu={_cpu_model()}"),
+    }
 
 
 def north_star(steps, warmup):
@@ -154,22 +192,130 @@ def north_star(steps, warmup):
     gbps = nbytes / (ms * 1e-3) / 1e9
     kgbps = nbytes / (kms * 1e-3) / 1e9
     return {"config": "2048x2048 fp16, D=256, k=11, window [H, W-D, D+1] forward (fast)",
+            "kernel": fwd_kernel_name("window", W, D),
             "voxels": nvox, "op_ms": round(ms, 4), "Mvoxels_per_s": round(nvox / (ms * 1e-3) / 1e6, 1),
             "achieved_GBps": round(gbps, 1), "frac_of_8TBps": round(gbps / HBM_PEAK_GBPS, 4),
             "sweep_kernel_ms": round(kms, 4), "sweep_kernel_GBps": round(kgbps, 1),
             "sweep_kernel_frac": round(kgbps / HBM_PEAK_GBPS, 4), "target_frac": 0.60}
 
 
+def config2_step(steps):
+    """configs[2] fwd+bwd at N = 1 (the previous rounds' headline workload), HIP events."""
+    import custereomatching_amd as cm
+
+    wl = WORKLOADS["c2"]
+    H, W, k, D = wl["H"], wl["W"], wl["k"], wl["D"]
+    cam, proj = synth_pair(H, W, D, 1000, "cuda")
+    cam.requires_grad_(True)
+    proj.requires_grad_(True)
+    g = torch.empty(H, W, W, device="cuda").uniform_(-1.0, 1.0)
+
+    def step():
+        cam.grad = None
+        proj.grad = None
+        cm.stereo_matching(cam, proj, D, k).backward(g)
+
+    step()
+    et = EventTimer()
+    for _ in range(steps):
+        et.record(step)
+    ms = et.mean_ms()
+    return {"config": wl["desc"], "ms_per_step": round(ms, 4),
+            "Mvoxels_per_s": round(H * W * W / (ms * 1e-3) / 1e6, 1)}
+
+
+def make_inputs(wl, rank, world, dev):
+    """Images (band of the global image for strong scaling; own image for weak) + upstream grad."""
+    from custereomatching_amd.rowband import band_bounds
+
+    H, W, D = wl["H"], wl["W"], wl["D"]
+    if wl["scaling"] == "strong":
+        cam, proj = synth_pair(H, W, D, 1000, "cpu", wl["dtype"])
+        b, e = band_bounds(H, world, rank)
+        cam, proj = cam[b:e].contiguous().to(dev), proj[b:e].contiguous().to(dev)
+    else:
+        cam, proj = synth_pair(H, W, D, 1000 + rank, dev, wl["dtype"])
+    rows = cam.shape[0]
+    WO, DO = (W, W) if wl["layout"] == "full" else (W - D, D + 1)
+    g = torch.empty(rows, WO, DO, device=dev)
+    g.uniform_(-1.0, 1.0, generator=torch.Generator(device=dev).manual_seed(7 + rank))
+    return cam, proj, g
+
+
+def pmc_child(args):
+    """Child of a rocprofv3 --pmc pass: the workload's dominant op, a few launches, nothing else."""
+    import custereomatching_amd as cm
+
+    wl = WORKLOADS[args.workload]
+    torch.cuda.set_device(0)
+    cam, proj, g = make_inputs(wl, 0, 1, torch.device("cuda", 0))
+    k, D, lay = wl["k"], wl["D"], wl["layout"]
+    vol = cm.cost_volume_forward(cam, proj, D, k, lay, args.precision)
+    for _ in range(3):
+        if args.pmc_child == "fwd":
+            cm.cost_volume_forward(cam, proj, D, k, lay, args.precision, out=vol)
+        else:
+            cm.cost_volume_backward(g, cam, proj, k, lay, D, camera_grad=True, projector_grad=True,
+                                    cost_volume=vol)
+    torch.cuda.synchronize()
+
+
+def pmc_traffic(args, which, kernel):
+    """HBM bytes per launch of `kernel`: two rocprofv3 passes over a child running the op
+    (FETCH_SIZE and WRITE_SIZE cannot share a pass; MI355X_MICROARCH.md §HBM/rocprofv3:
+    both in KiB, FETCH_SIZE reports half the bytes on gfx950 -> x2048 and x1024 B/unit)."""
+    out = tempfile.mkdtemp(prefix="custma_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    vals = {}
+    for counter, scale in (("FETCH_SIZE", 2048.0), ("WRITE_SIZE", 1024.0)):
+        d = os.path.join(out, counter)
+        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", counter, "-d", d, "-o", "run",
+               "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--workload",
+               args.workload, "--precision", args.precision, "--pmc-child", which]
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
+        if r.returncode != 0:
+            return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode}): {r.stderr[-300:]}"
+        xs = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                    xs.append(float(row["Counter_Value"]))
+        if not xs:
+            return None, f"no {counter} samples for {kernel}"
+        vals[counter] = sum(xs) / len(xs) * scale
+    src = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate) over `bench.py --pmc-child {which}` "
+           f"(same workload), mean per {kernel} launch; FETCH x2048 B, WRITE x1024 B per unit")
+    return {"read": vals["FETCH_SIZE"], "write": vals["WRITE_SIZE"],
+            "total": vals["FETCH_SIZE"] + vals["WRITE_SIZE"]}, src
+
+
 def main():
     args = parse()
+    if args.pmc_child:
+        pmc_child(args)
+        return
     world = args.gpus
+    if world > 1 and "RANK" not in os.environ:
+        # no launcher: start one (child process; nothing has touched the GPU yet) and pass its status on
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+               *sys.argv[1:]]
+        sys.exit(subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode)
+
+    import torch.distributed as dist
+
     distributed = world > 1
     if distributed:
         rank = int(os.environ["RANK"])
         local = int(os.environ.get("LOCAL_RANK", rank))
-        torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
     else:
         rank, local = 0, 0
         torch.cuda.set_device(0)
@@ -179,26 +325,23 @@ def main():
     from custereomatching_amd import _lib
     from custereomatching_amd.rowband import stereo_matching_rowband
 
-    H, W, k, D = args.H, args.W, args.k, args.D
-    cam, proj = synth_pair(H, W, D, 1000 + rank, dev)
+    wl = WORKLOADS[args.workload]
+    H, W, k, D, layout = wl["H"], wl["W"], wl["k"], wl["D"], wl["layout"]
+    cam, proj, g = make_inputs(wl, rank, world, dev)
     cam.requires_grad_(True)
     proj.requires_grad_(True)
-    WO = W if args.layout == "full" else W - D
-    DO = W if args.layout == "full" else D + 1
-    g = torch.empty(H, WO, DO, device=dev)
-    g.uniform_(-1.0, 1.0, generator=torch.Generator(device=dev).manual_seed(7 + rank))
+    global_H = H if wl["scaling"] == "strong" else H * world
 
     def op():
         if distributed:
-            return stereo_matching_rowband(cam, proj, D, k, args.layout, args.precision)
-        return cm.stereo_matching(cam, proj, D, k, args.layout, args.precision)
+            return stereo_matching_rowband(cam, proj, D, k, layout, args.precision, H=global_H)
+        return cm.stereo_matching(cam, proj, D, k, layout, args.precision)
 
     def step():
         cam.grad = None
         proj.grad = None
         vol = op()
         vol.backward(g)
-        return vol
 
     for _ in range(args.warmup):
         step()
@@ -220,52 +363,40 @@ def main():
     fwd_kms, n_fk = _lib.profile_mean_ms(_lib.PROF_FWD)
     bwd_kms, n_bk = _lib.profile_mean_ms(_lib.PROF_BWD)
     _lib.profile_enable(False)
+    rows = cam.shape[0]
+    WO, DO = (W, W) if layout == "full" else (W - D, D + 1)
+    nvox_rank = rows * WO * DO
+    tot = torch.tensor([elapsed, float(nvox_rank)], dtype=torch.float64,
+                       device=dev if args.dist_backend == "nccl" else "cpu")
     if distributed:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    nvox_rank = H * WO * DO
-    value = world * nvox_rank * args.steps / elapsed / 1e6
+        t_max = tot[:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        v_sum = tot[1:].clone()
+        dist.all_reduce(v_sum, op=dist.ReduceOp.SUM)
+        elapsed, nvox_all = float(t_max.item()), float(v_sum.item())
+    else:
+        nvox_all = float(nvox_rank)
+    value = nvox_all * args.steps / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
 
-    # Per-op HIP-event timing (same stream as the kernels), outside the timed region.
-    et_f, et_b = EventTimer(), EventTimer()
-    vol = cm.cost_volume_forward(cam.detach(), proj.detach(), D, k, args.layout, args.precision)
-    for _ in range(max(3, args.steps // 2)):
-        with torch.no_grad():
-            et_f.record(lambda: cm.cost_volume_forward(cam.detach(), proj.detach(), D, k, args.layout,
-                                                       args.precision, out=vol))
-        et_b.record(lambda: cm.cost_volume_backward(g, cam.detach(), proj.detach(), k, args.layout, D,
-                                                    camera_grad=True, projector_grad=True, cost_volume=vol))
-    del vol
-    fwd_ms, bwd_ms = et_f.mean_ms(), et_b.mean_ms()
-    # Algorithmic bytes per launch:
+    # Algorithmic bytes per launch, this rank's band:
     #   forward sweep  : volume written once + both images read
     #   backward sweep : upstream gradient + saved volume read once each, both images read,
-    #                    both image gradients written
-    img = 2 * H * W * 4
+    #                    both image gradients written (fp32)
+    esz = cam.element_size()
+    img = 2 * cam.numel() * esz
     fwd_bytes = nvox_rank * 4 + img
-    bwd_bytes = 2 * nvox_rank * 4 + img + img
-    # forward sweep kernel by layout (sweep_wave.hip launch_fwd_fast): full -> k_sweep_fwd, window -> k_fwd_wave
-    fwd_name = "k_sweep_fwd" if args.layout == "full" else "k_fwd_wave"
+    bwd_bytes = 2 * nvox_rank * 4 + img + 2 * cam.numel() * 4
+    fwd_name = fwd_kernel_name(layout, W, D)
     kern = {
         fwd_name: {"avg_launch_ms": round(fwd_kms, 4), "launches": n_fk, "algorithmic_bytes": fwd_bytes,
-                        "achieved_GBps": round(fwd_bytes / (fwd_kms * 1e-3) / 1e9, 1) if fwd_kms else None},
+                   "achieved_GBps": round(fwd_bytes / (fwd_kms * 1e-3) / 1e9, 1) if fwd_kms else None},
         "k_bwd_coop": {"avg_launch_ms": round(bwd_kms, 4), "launches": n_bk, "algorithmic_bytes": bwd_bytes,
-                        "achieved_GBps": round(bwd_bytes / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None},
+                       "achieved_GBps": round(bwd_bytes / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None},
     }
     dom = "k_bwd_coop" if bwd_kms >= fwd_kms else fwd_name
     dk = kern[dom]
     achieved = dk["achieved_GBps"] or 0.0
-
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{dom}_c2_{args.layout}.json")
-    if os.path.exists(pmc_path):
-        try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
-
     result = {
         "metric": "cost-volume Mvoxels/s (H x W x D) fwd+bwd",
         "value": round(value, 1),
@@ -275,16 +406,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl["scaling"],
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f16" if wl["dtype"] == torch.float16 else "f32",
         "data": "synthetic (seeded speckle pair, camera = shifted projector + noise; uniform upstream grad)",
         "config": {
-            "workload": ("BASELINE configs[2]: fwd+bwd (grads wrt both images) of the reference op's "
-                         f"{args.layout} volume, {H}x{W} fp32 pair per GPU, D={D}, window k={k}"),
-            "H_per_gpu": H, "W": W, "k": k, "D": D, "layout": args.layout, "precision": args.precision,
-            "voxels_per_gpu_per_step": nvox_rank, "global_H": H * world,
+            "workload": wl["desc"],
+            "H": global_H, "W": W, "k": k, "D": D, "layout": layout, "precision": args.precision,
+            "rows_per_gpu": rows, "voxels_per_step": int(nvox_all),
             "parallelism": f"rowband{world}" if distributed else "single",
+            "dist_backend": args.dist_backend if distributed else None,
         },
         "roofline": {
             "bound": "hbm",
@@ -293,24 +424,31 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": traffic,
+            "traffic": None,
             "algorithmic_bytes_per_launch": dk["algorithmic_bytes"],
             "avg_launch_ms": dk["avg_launch_ms"],
             "timing": "HIP events around each launch of the kernel on the op's stream, over the timed steps",
         },
         "kernels": kern,
-        "breakdown": {
-            "fwd_op_ms": round(fwd_ms, 4), "bwd_op_ms": round(bwd_ms, 4),
-            "fwd_Mvox_s": round(nvox_rank / (fwd_ms * 1e-3) / 1e6, 1),
-            "bwd_Mvox_s": round(nvox_rank / (bwd_ms * 1e-3) / 1e6, 1),
-        },
     }
     del g
+    cam.grad = proj.grad = None
     torch.cuda.empty_cache()
-    if rank == 0 and world == 1 and not args.no_north_star:
-        result["north_star"] = north_star(max(5, args.steps), 2)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, k)
+    if rank == 0 and world == 1:
+        if not args.no_north_star:
+            result["north_star"] = north_star(max(5, args.steps), 2)
+        if not args.no_config2 and args.workload != "c2":
+            result["config2"] = config2_step(max(5, args.steps // 2))
+        torch.cuda.empty_cache()
+        if not args.no_pmc:
+            traffic, src = pmc_traffic(args, "bwd" if dom == "k_bwd_coop" else "fwd", dom)
+            if traffic is not None:
+                result["roofline"]["traffic"] = round(traffic["total"])
+                result["roofline"]["traffic_read"] = round(traffic["read"])
+                result["roofline"]["traffic_write"] = round(traffic["write"])
+            result["roofline"]["traffic_source"] = src
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(wl, args.cpu_rows or (48 if layout == "window" else 96))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:

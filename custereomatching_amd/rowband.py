@@ -92,6 +92,23 @@ class RowBandGroup:
     def _peer(self, rank):
         return dist.get_global_rank(self.group, rank) if self.group is not None else rank
 
+    def _p2p(self, sends, recvs):
+        """One batch_isend_irecv of (tensor, group rank) pairs.  Device tensors on a gloo
+        group (CPU-only transport, e.g. a single-GPU rehearsal) are staged through host
+        memory; with nccl (RCCL over xGMI) they go device to device."""
+        stage = dist.get_backend(self.group) == "gloo" and any(t.is_cuda for t, _ in sends + recvs)
+        hs = [(t.cpu() if stage else t, q) for t, q in sends]
+        hr = [(torch.empty(t.shape, dtype=t.dtype) if stage else t, q) for t, q in recvs]
+        # zero-row parts (k = 2: no rows below the patch centre) are not sent at all
+        ops = [dist.P2POp(dist.isend, t.contiguous(), self._peer(q), self.group) for t, q in hs if t.numel()]
+        ops += [dist.P2POp(dist.irecv, t, self._peer(q), self.group) for t, q in hr if t.numel()]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        if stage:
+            for (dst, _), (src, _) in zip(recvs, hr):
+                dst.copy_(src)
+
     def halo_sizes(self) -> Tuple[int, int]:
         """Rows received from the rank above (o) and from the rank below (a)."""
         top = self.o if self.rank > 0 else 0
@@ -101,23 +118,22 @@ class RowBandGroup:
     def exchange_halo(self, band: torch.Tensor) -> torch.Tensor:
         """[n, W] owned rows -> [top + n + bot, W] with the neighbours' edge rows."""
         top, bot = self.halo_sizes()
-        if top == 0 and bot == 0:
+        if self.world == 1 or self.o + self.a == 0:
             return band
         n = band.shape[0]
         if n < max(self.o, self.a):
             raise ValueError(f"row band of {n} rows is thinner than the halo ({self.o} / {self.a} rows)")
         out = torch.empty((top + n + bot,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
         out[top:top + n].copy_(band)
-        ops = []
+        sends, recvs = [], []
         # the rank above needs my first a rows (its bottom halo); the rank below my last o rows
-        if top:
-            ops.append(dist.P2POp(dist.isend, band[:self.a].contiguous(), self._peer(self.rank - 1), self.group))
-            ops.append(dist.P2POp(dist.irecv, out[:top], self._peer(self.rank - 1), self.group))
-        if bot:
-            ops.append(dist.P2POp(dist.isend, band[n - self.o:].contiguous(), self._peer(self.rank + 1), self.group))
-            ops.append(dist.P2POp(dist.irecv, out[top + n:], self._peer(self.rank + 1), self.group))
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+        if self.rank > 0:
+            sends.append((band[:self.a], self.rank - 1))
+            recvs.append((out[:top], self.rank - 1))
+        if self.rank < self.world - 1:
+            sends.append((band[n - self.o:], self.rank + 1))
+            recvs.append((out[top + n:], self.rank + 1))
+        self._p2p(sends, recvs)
         return out
 
     def reduce_halo(self, buf: torch.Tensor, n: int) -> torch.Tensor:
@@ -126,24 +142,23 @@ class RowBandGroup:
         rows this rank owns)."""
         top, bot = self.halo_sizes()
         own = buf[top:top + n]
-        if top == 0 and bot == 0:
+        if self.world == 1 or self.o + self.a == 0:
             return own.contiguous()
         own = own.clone()
-        ops = []
+        sends, recvs = [], []
         # partials of my first a rows come from the rank above, of my last o rows from the rank below
-        from_up = torch.empty((self.a,) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device) if top else None
-        from_dn = torch.empty((self.o,) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device) if bot else None
-        if top:
-            ops.append(dist.P2POp(dist.isend, buf[:top].contiguous(), self._peer(self.rank - 1), self.group))
-            ops.append(dist.P2POp(dist.irecv, from_up, self._peer(self.rank - 1), self.group))
-        if bot:
-            ops.append(dist.P2POp(dist.isend, buf[top + n:].contiguous(), self._peer(self.rank + 1), self.group))
-            ops.append(dist.P2POp(dist.irecv, from_dn, self._peer(self.rank + 1), self.group))
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-        if top and self.a:
+        from_up = torch.empty((self.a,) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device)
+        from_dn = torch.empty((self.o,) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device)
+        if self.rank > 0:
+            sends.append((buf[:top], self.rank - 1))
+            recvs.append((from_up, self.rank - 1))
+        if self.rank < self.world - 1:
+            sends.append((buf[top + n:], self.rank + 1))
+            recvs.append((from_dn, self.rank + 1))
+        self._p2p(sends, recvs)
+        if self.rank > 0 and self.a:
             own[:self.a] += from_up
-        if bot and self.o:
+        if self.rank < self.world - 1 and self.o:
             own[n - self.o:] += from_dn
         return own
 

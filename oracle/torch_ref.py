@@ -44,18 +44,45 @@ def cost_volume(cam: torch.Tensor, proj: torch.Tensor, k: int) -> torch.Tensor:
     return (exy + EPS) / torch.sqrt(ex2 * ey2 + EPS)
 
 
-def forward_backward(cam, proj, k, grad=None, proj_grad=True, row_chunk=None):
+def window_cost_volume(cam: torch.Tensor, proj: torch.Tensor, k: int, D: int, block: int = 256) -> torch.Tensor:
+    """Window layout [H, W-D, D+1], out[h, w, s] = full[h, w, w+s]: the same centred
+    patches, EXY by bmm and ZNCC as cost_volume, with the bmm taken per block of
+    `block` camera columns against the block + D projector columns it can reach and
+    the window's diagonals read out of each product (the full [W, W] bmm would
+    compute W / (D+1) times more than the window holds)."""
+    pc = patches(cam, k)
+    pp = patches(proj, k)
+    pc = pc - pc.mean(dim=-1, keepdim=True)
+    pp = pp - pp.mean(dim=-1, keepdim=True)
+    H, W = cam.shape
+    WO = W - D
+    ex2 = (pc * pc).sum(-1)
+    ey2 = (pp * pp).sum(-1)
+    outs = []
+    for w0 in range(0, WO, block):
+        b = min(block, WO - w0)
+        exy = torch.bmm(pc[:, w0:w0 + b], pp[:, w0:w0 + b + D].transpose(1, 2))  # [H, b, b + D]
+        # diagonal band: band[h, w, s] = exy[h, w, w + s]
+        band = exy.as_strided((H, b, D + 1), (exy.stride(0), exy.stride(1) + 1, 1), exy.storage_offset())
+        den = torch.sqrt(ex2[:, w0:w0 + b, None] * ey2[:, w0:w0 + b + D].unfold(1, D + 1, 1) + EPS)
+        outs.append((band + EPS) / den)
+    return torch.cat(outs, dim=1)
+
+
+def forward_backward(cam, proj, k, grad=None, proj_grad=True, row_chunk=None, layout="full", D=0):
     """Returns (volume, camera_grad, projector_grad) on CPU.
 
     grad=None means ones (verify.py:123).  With row_chunk the volume is not
-    returned (None) and gradients are accumulated band by band.
+    returned (None) and gradients are accumulated band by band.  layout="window"
+    uses window_cost_volume.
     """
+    vol_fn = cost_volume if layout == "full" else (lambda c, p, kk: window_cost_volume(c, p, kk, D))
     H, W = cam.shape
     o, a_ = k // 2, k - 1 - k // 2  # halo rows above / below a band
     if row_chunk is None or row_chunk >= H:
         c = cam.detach().clone().requires_grad_(True)
         p = proj.detach().clone().requires_grad_(proj_grad)
-        v = cost_volume(c, p, k)
+        v = vol_fn(c, p, k)
         v.backward(torch.ones_like(v) if grad is None else grad)
         return v.detach(), c.grad, (p.grad if proj_grad else None)
     gc = torch.zeros_like(cam)
@@ -65,24 +92,16 @@ def forward_backward(cam, proj, k, grad=None, proj_grad=True, row_chunk=None):
         a0, a1 = max(0, h0 - o), min(H, h1 + a_)
         c = cam[a0:a1].detach().clone().requires_grad_(True)
         p = proj[a0:a1].detach().clone().requires_grad_(proj_grad)
-        # The band's own zero padding differs from the image's at interior
-        # band edges, so compute on the haloed band and keep rows h0..h1.
-        v = band_volume(c, p, k, h0 - a0, h1 - a0, top_pad=(a0 == 0), bot_pad=(a1 == H))
+        # Rows outside the band that exist in the full image are present as halo, so only
+        # true image borders are zero padded; the band's own (wrong) edge padding only
+        # feeds volume rows outside h0..h1, which are dropped.
+        v = vol_fn(c, p, k)[h0 - a0:h1 - a0]
         g = torch.ones_like(v) if grad is None else grad[h0:h1]
         v.backward(g)
         gc[a0:a1] += c.grad
         if proj_grad:
             gp[a0:a1] += p.grad
     return None, gc, (gp if proj_grad else None)
-
-
-def band_volume(c, p, k, o0, o1, top_pad, bot_pad):
-    """Volume rows o0..o1 of a haloed band.  Rows outside the band that exist
-    in the full image are present in c/p as halo, so only true image borders
-    are zero padded (F.pad on the band pads halo edges too, but those padded
-    rows only feed output rows outside o0..o1)."""
-    v = cost_volume(c, p, k)
-    return v[o0:o1]
 
 
 def forward_only(cam, proj, k, row_chunk=None):

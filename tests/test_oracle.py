@@ -164,3 +164,21 @@ def test_torch_ref_even_k_matches_c_oracle(k):
     assert np.abs(v.numpy() - O.forward_f64(cam, proj, k)).max() <= 1e-9
     assert np.abs(gc.numpy() - rc).max() <= 1e-9 * max(1.0, np.abs(rc).max())
     assert np.abs(gp.numpy() - rp).max() <= 1e-9 * max(1.0, np.abs(rp).max())
+
+
+@pytest.mark.parametrize("k,D,row_chunk", [(5, 7, None), (11, 12, 5), (4, 3, 4)])
+def test_torch_ref_window_layout_matches_c_oracle(k, D, row_chunk):
+    """The window-layout CPU baseline (bench.py's c5 workload) against the C oracle."""
+    import torch
+
+    from oracle import torch_ref as T
+
+    cam, proj = make_pair(16, 40, D, seed=k + D)
+    g = np.random.default_rng(1).standard_normal((16, 40 - D, D + 1)).astype(np.float32)
+    v, gc, gp = T.forward_backward(torch.from_numpy(cam).double(), torch.from_numpy(proj).double(), k,
+                                   grad=torch.from_numpy(g).double(), layout="window", D=D, row_chunk=row_chunk)
+    rc, rp = O.backward_f64(g, cam, proj, k, layout=O.WINDOW, D=D)
+    if v is not None:
+        assert np.abs(v.numpy() - O.forward_f64(cam, proj, k, layout=O.WINDOW, D=D)).max() <= 1e-9
+    assert np.abs(gc.numpy() - rc).max() <= 1e-9 * max(1.0, np.abs(rc).max())
+    assert np.abs(gp.numpy() - rp).max() <= 1e-9 * max(1.0, np.abs(rp).max())

@@ -89,7 +89,7 @@ def _run(world, H, W, k, D, layout, pass_h=False):
 
 
 @pytest.mark.parametrize("world,layout,k", [(2, "full", 5), (3, "window", 5), (2, "window", 5), (2, "full", 4),
-                                            (3, "window", 6)])
+                                            (3, "window", 6), (2, "full", 2), (3, "full", 1)])
 def test_rowband_matches_single_device(world, layout, k):
     """Odd k: r halo rows each side; even k: k/2 rows from the rank above, k/2-1 from below."""
     H, W, D = 23, 28, 6
