@@ -74,13 +74,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
-def build_variant(libdir: str, defines) -> str:
-    """Ablation build (benchmarking only): the same library compiled with extra
-    -D switches into another directory; load it with CUSTMA_LIB=<path>."""
+def build_variant(libdir: str, defines, only=None) -> str:
+    """Ablation build (benchmarking only): the same library with extra -D switches into
+    another directory; load it with CUSTMA_LIB=<path>.  `only`: the translation units the
+    switches affect (the rest link from the main build's objects)."""
     os.makedirs(libdir, exist_ok=True)
     extra = [f"-D{d}" for d in defines]
-    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, extra, libdir), SOURCES))
+    todo = [s for s in SOURCES if only is None or s in only]
+    if only is not None:
+        build()
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(len(todo), os.cpu_count() or 4))) as ex:
+        done = dict(zip(todo, ex.map(lambda s: _compile(s, extra, libdir), todo)))
+    objs = [done.get(s, _obj(s)) for s in SOURCES]
     lib = os.path.join(libdir, "libcustma_hip.so")
     r = subprocess.run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", lib, *objs], capture_output=True, text=True)
     if r.returncode != 0:

@@ -51,9 +51,11 @@ namespace custma {
 
 namespace {
 
-constexpr int TRB = 16;   // own rows per wave
+#ifndef CUSTMA_BWD_ROWS
+#define CUSTMA_BWD_ROWS 16
+#endif
+constexpr int TRB = CUSTMA_BWD_ROWS;  // own rows per unit (workgroup)
 constexpr int NLB = 64;   // diagonals per wave
-constexpr int FB = 16;    // steps per flush
 constexpr int NTYPE = 6;  // partial types: T1c, Am, B (camera) | T1p, Ac, Bp (projector)
 constexpr int kSeg = 128; // pixel columns per wave (>= 64 + 2 r: segments s and s+2 never overlap)
 constexpr uint32_t kOOB = 0x80000000u;
@@ -147,313 +149,25 @@ __device__ __forceinline__ int chunk_of_rank(int r, int n, int jc) {
     return above > below ? jc + m + rest : jc - m - rest;
 }
 
-template <int K>
-__device__ __forceinline__ void bwd_sweep_body(const Geo& g, const BwdArgs& a, int j, int sg, int rg,
-                                               float (*cbuf)[48], float (*pbuf)[48]) {
-    constexpr int R = K / 2, NY = TRB + 2 * R;
-    static_assert(NY <= 32, "two row-replicated registers cover the rows");
-
-    const ChunkGeo cg = chunk_geo(g, a.dlo, j);
-    const int lane = threadIdx.x;
-    // lane-level index math in 32 bits (images and one volume row slab < 2 GiB: backward_supported)
-    const int Wi = (int)g.W, Hi = (int)g.H;
-    const int d0 = (int)cg.d0, dl = d0 + lane;
-    const int64_t y0 = a.ylo + (int64_t)TRB * rg;
-    const int y0i = (int)y0;
-    int64_t xs64, xe64;  // output pixel columns of this segment; sweep steps w in [w0, wend)
-    seg_cols(cg, R, sg, &xs64, &xe64);
-    const int xs = (int)xs64, xe = (int)xe64;
-    const int w0 = xs - R, wend = xe + R;
-    const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
-    // this lane's voxel columns [lwlo, lwhi)
-    int lwlo, lwhi;
-    if (window) {
-        lwlo = 0;
-        lwhi = (dl >= 0 && dl <= g.D) ? (int)g.WO : 0;
-    } else {
-        lwlo = dl < 0 ? -dl : 0;
-        lwhi = min((int)g.WO, Wi - dl);
-    }
-    const int gsU = (int)g.DO + (window ? 0 : 1);
-    const int slot = 2 * (j % a.Sj) + (sg & 1);
-    const size_t plane = (size_t)g.H * g.W;
-    const float cb = a.shift[0], pb = a.shift[1];
-
-    // Descriptors: whole fp32 images (< 2 GiB, checked on the host) and the volume from the
-    // wave's first volume row; rows are selected with a wave-uniform soffset, columns and
-    // lane validity with the per-lane voffset (0x80000000 = out of range = 0).
-    const uint32_t ib = (uint32_t)(plane * 4);
-    const auto rXc = make_rsrc(a.Xc, ib), rMc = make_rsrc(a.mcc, ib), rCc = make_rsrc(a.cc, ib);
-    const auto rYp = make_rsrc(a.Yp, ib), rMp = make_rsrc(a.mpp, ib), rPp = make_rsrc(a.pp, ib);
-    const size_t slab = (size_t)g.WO * g.DO;  // volume floats per row
-    const int64_t vrow0 = max(g.h_lo, y0 - R);  // first volume row this wave reads
-    const auto rG = make_rsrc(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
-    const auto rV = make_rsrc(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
-    // (voffset + soffset stays below 0x7FFFFFF0 for in-volume rows: backward_supported)
-
-    // soffset of row y0 - R + y: image rows clamped into the image (values of clamped rows
-    // only ever multiply a zero gradient or feed outputs that are not stored), volume rows
-    // relative to vrow0 (rows outside the volume only in EDGE waves, where they are masked)
-    const int64_t ir0 = y0 - R;
-    const uint32_t vstride = (uint32_t)(slab * 4);
-    const int hlo = (int)g.h_lo, hhi = (int)g.h_hi, vrow0i = (int)vrow0;
-    auto img_off = [&](int row, int col) -> uint32_t {
-        return (row >= 0 && row < Hi && col >= 0 && col < Wi) ? (uint32_t)((row * Wi + col) * 4) : kOOB;
-    };
-    auto col_off = [&](int col) -> uint32_t { return (col >= 0 && col < Wi) ? (uint32_t)(col * 4) : kOOB; };
-
-    float HA[NY];
-#pragma unroll
-    for (int y = 0; y < NY; ++y) HA[y] = 0.f;
-    float P[3][TRB];  // projector accumulators: T1p, Ac, Bp
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-#pragma unroll
-        for (int m = 0; m < TRB; ++m) P[t][m] = 0.f;
-
-    const int m16 = lane & 15;
-    // Partial planes of this wave: type t, slot, rows [y0, y0 + 16) (rows past yhi out of range)
-    const uint32_t prow_bytes = (uint32_t)(min((int64_t)TRB, a.yhi - y0) * g.W * 4);
-    auto part_rsrc = [&](int t) {
-        return make_rsrc(a.part + ((size_t)t * a.S + slot) * plane + (size_t)y0 * g.W, prow_bytes);
-    };
-    auto flush = [&](int wfirst, int nsteps) {
-        // pair p = type*16 + m; step jcol of the buffer = column wfirst + jcol.  The lane
-        // index is made opaque so the per-lane store offsets are formed here, not hoisted
-        // out of the sweep (they would pin ~50 VGPRs).
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const int jcol = ln & 15, pg = ln >> 4;
-        const bool live = jcol < nsteps;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            const int t = i >> 2, p = pg + 4 * i, m = p & 15;  // t is uniform per i
-            const int col = wfirst + jcol - (t == 0 ? R : 0);
-            const bool cok = live && col >= xs && col < xe && col >= 0 && col < Wi;
-            const uint32_t off = cok ? (uint32_t)((m * Wi + col) * 4) : kOOB;
-            st_buf(cbuf[jcol][p], part_rsrc(t), off);
-            // projector saves: column (w - 1 + off + d0) for the step at w
-            const int pcol = wfirst + jcol - 1 + (t == 0 ? -R : 0) + d0;
-            const uint32_t poff = (live && pcol >= 0 && pcol < Wi) ? (uint32_t)((m * Wi + pcol) * 4) : kOOB;
-            st_buf(pbuf[jcol][p], part_rsrc(3 + t), poff);
-        }
-    };
-
-    // Camera-side sums: pairs are folded across lanes as soon as both members exist
-    // (am,b of one row: permlane32; two rows: permlane16; T1c rows likewise), so at most
-    // 12 partly reduced registers are live; reduce_tail12 finishes them.  Which of the 48
-    // sums (type*16 + row) a lane ends up with is found once by running the same tree on
-    // the sums' indices placed in lane 0.
-    float wA[12];
-    auto cam_reduce = [&](auto&& am, auto&& b, auto&& t1) -> float {
-        Unroll<0, TRB / 2>::run([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            wA[i] = red16(red32(am(2 * i), b(2 * i)), red32(am(2 * i + 1), b(2 * i + 1)));
-        });
-        Unroll<0, TRB / 4>::run([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            wA[8 + i] = red16(red32(t1(4 * i), t1(4 * i + 1)), red32(t1(4 * i + 2), t1(4 * i + 3)));
-        });
-        return reduce_tail12(wA, lane);
-    };
-    int qlane;
-    {
-        const bool l0 = lane == 0;
-        qlane = (int)cam_reduce([&](int m) { return l0 ? (float)(16 + m) : 0.f; },
-                                [&](int m) { return l0 ? (float)(32 + m) : 0.f; },
-                                [&](int m) { return l0 ? (float)m : 0.f; });
-    }
-
-    for (int wfirst = w0; wfirst < wend; wfirst += FB) {
-    const int nsteps = min(FB, wend - wfirst);
-#pragma unroll 1
-    for (int s = 0; s < nsteps; ++s) {
-        const int w = wfirst + s;
-        // ---- emit lane 0 of the projector accumulators (their completed column)
-        if (lane == 0) {
-#pragma unroll
-            for (int t = 0; t < 3; ++t)
-#pragma unroll
-                for (int m = 0; m < TRB; m += 4)
-                    *(float4*)&pbuf[s][t * 16 + m] = make_float4(P[t][m], P[t][m + 1], P[t][m + 2], P[t][m + 3]);
-        }
-        const int xb = w - R;  // pixel column whose box is complete this step
-        const int wl = w - K;  // column leaving the horizontal window
-        // the leaving column was added only if it is a step of this sweep
-        const bool ve = w >= lwlo && w < lwhi, vl = wl >= lwlo && wl < lwhi && wl >= w0;
-        // contributions of this segment only: T1 for pixel columns in [xs, xe) (the first
-        // 2r steps only fill the box), per-voxel terms for camera columns in [xs, xe)
-        const float tf = xb >= xs ? 1.f : 0.f, af = (w >= xs && w < xe) ? 1.f : 0.f;
-        const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
-        const uint32_t oGl = vl ? (uint32_t)((wl * gsU + dl) * 4) : kOOB;
-        const uint32_t oYe = col_off(w + dl), oYl = col_off(wl + dl), oPq = col_off(xb + dl);
-        // row-replicated per-row values (lane i: row y = 16 h + (i & 15) of the NY rows)
-        float xe[2], xl[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int row = (int)ir0 + 16 * h + m16;
-            const bool rok = 16 * h + m16 < NY;
-            xe[h] = ld_buf<float>(rXc, rok ? img_off(row, w) : kOOB);
-            xl[h] = ld_buf<float>(rXc, rok ? img_off(row, wl) : kOOB);
-        }
-        // own rows: mc'(y0+m, w), c'(y0+m, xb)
-        const float mco = ld_buf<float>(rMc, img_off(y0i + m16, w)) * af;
-        const float cxo = (ld_buf<float>(rCc, img_off(y0i + m16, xb)) - cb) * tf;
-        // Row offsets, rebuilt every step (keeps them out of the loop-invariant SGPR set).
-        // Image rows are clamped into the image (a clamped row's values only multiply a zero
-        // gradient or feed outputs that are not stored).  The range check includes soffset
-        // (gfx950, scripts/micro/soffset_test.hip): a row outside the volume gets an soffset
-        // past the descriptor's end and reads zeros.
-        int ir = (int)ir0;
-        asm volatile("" : "+s"(ir));
-        auto iso = [&](int y) -> uint32_t {
-            int rr = ir + y;
-            rr = rr < 0 ? 0 : rr >= Hi ? Hi - 1 : rr;
-            return (uint32_t)rr * (uint32_t)(Wi * 4);
-        };
-        auto vso = [&](int y) -> uint32_t {
-            const int row = ir + y;
-            return (row >= hlo && row < hhi) ? (uint32_t)(row - vrow0i) * vstride : 0x7FFFFFF0u;
-        };
-
-        // ---- A entering (column w) and leaving (column w - k) on the NY rows; the loads of
-        // row y + kPF are issued before row y is computed (sched barriers keep that order and
-        // stop the scheduler from hoisting all rows' loads, which would pin ~150 VGPRs)
-        struct RowLd {
-            float ge, gl, Ye, Yl, cv, mp;
-        };
-        RowLd rl[NY];
-        auto issue = [&](auto yc) {
-            constexpr int y = decltype(yc)::value;
-            const uint32_t so = vso(y), sy = iso(y);
-            rl[y].ge = ld_vol(rG, oGe, so);
-#ifndef CUSTMA_ABL_NOLEAVE  // ablation builds only (scripts/build_ablations.py)
-            rl[y].gl = ld_vol(rG, oGl, so);
-#else
-            rl[y].gl = 0.f;
-#endif
-#ifndef CUSTMA_ABL_NOIMG
-            rl[y].Ye = ld_bufs<float>(rYp, oYe, sy);
-            rl[y].Yl = ld_bufs<float>(rYp, oYl, sy);
-#else
-            rl[y].Ye = 1.f + (float)y;
-            rl[y].Yl = 1.f;
-#endif
-            if constexpr (y >= R && y < R + TRB) {
-                rl[y].cv = ld_vol(rV, oGe, so);
-#ifndef CUSTMA_ABL_NOIMG
-                rl[y].mp = ld_bufs<float>(rMp, oYe, sy);
-#else
-                rl[y].mp = 0.5f;
-#endif
-            }
-        };
-        Unroll<0, (kPF < NY ? kPF : NY)>::run([&](auto yc) { issue(yc); });
-        float amv[TRB], bv[TRB];
-        Unroll<0, NY>::run([&](auto yc) {
-            constexpr int y = decltype(yc)::value;
-            if constexpr (y + kPF < NY) issue(std::integral_constant<int, y + kPF>{});
-            const RowLd& L = rl[y];
-            const float Xe = bcast<y & 15>(xe[y >> 4]), Xl = bcast<y & 15>(xl[y >> 4]);
-            const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xe, L.Ye, kEps));
-            const float rSl = __builtin_amdgcn_rsqf(__builtin_fmaf(Xl, L.Yl, kEps));
-            const float Ae = L.ge * rSe, Al = L.gl * rSl;
-            HA[y] += Ae - Al;
-            if constexpr (y >= R && y < R + TRB) {
-                constexpr int m = y - R;
-                const float V = Ae * L.cv * rSe;
-                amv[m] = Ae * L.mp;
-                bv[m] = V * L.Ye;
-                P[1][m] = shl1_add(P[1][m], Ae * bcast<m>(mco));
-                P[2][m] = shl1_add(P[2][m], (V * af) * Xe);
-                if constexpr (m & 1)  // fold the row pair (m-1, m) of Am and B
-                    wA[m / 2] = red16(red32(amv[m - 1], bv[m - 1]), red32(amv[m], bv[m]));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        });
-        // ---- vertical box over the registers: BoxA for the 16 own rows at pixel column xb
-        float pq[TRB];
-        Unroll<0, 4>::run([&](auto mc) {
-            constexpr int m = decltype(mc)::value;
-            pq[m] = ld_bufs<float>(rPp, oPq, iso(R + m));
-        });
-        float bx = 0.f;
-#pragma unroll
-        for (int y = 0; y <= 2 * R; ++y) bx += HA[y];
-        float t1v[TRB];
-        Unroll<0, TRB>::run([&](auto mc) {
-            constexpr int m = decltype(mc)::value;
-            if constexpr (m + 4 < TRB) pq[m + 4] = ld_bufs<float>(rPp, oPq, iso(R + m + 4));
-            if constexpr (m > 0) bx = (bx + HA[m + 2 * R]) - HA[m - 1];
-            t1v[m] = (pq[m] - pb) * bx;  // p'(y0+m, xb+dl) BoxA
-            P[0][m] = shl1_add(P[0][m], bcast<m>(cxo) * bx);
-            if constexpr ((m & 3) == 3)
-                wA[8 + m / 4] = red16(red32(t1v[m - 3], t1v[m - 2]), red32(t1v[m - 1], t1v[m]));
-            __builtin_amdgcn_sched_barrier(0);
-        });
-#ifndef CUSTMA_ABL_NORED
-        const float red = reduce_tail12(wA, lane);
-#else
-        float red = 0.f;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) red += wA[i];
-#endif
-        cbuf[s][qlane] = red;
-    }
-    __syncthreads();
-    flush(wfirst, nsteps);
-    __syncthreads();
-    }
-    // ---- final projector state: lane l holds column (wend - 1) + off + d0 + l
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-        const int col = wend - 1 + (t == 0 ? -R : 0) + d0 + lane;
-        const uint32_t c4 = (col >= 0 && col < g.W) ? (uint32_t)(col * 4) : kOOB;
-        const auto rp = part_rsrc(3 + t);
-#pragma unroll
-        for (int m = 0; m < TRB; ++m)
-            st_buf(P[t][m], rp, c4 == kOOB ? kOOB : c4 + (uint32_t)(m * Wi * 4));
-    }
-}
-
-template <int K>
-__global__ __launch_bounds__(64) void k_bwd_sweep(Geo g, BwdArgs a) {
-    // Block order: XCD x (hardware block b runs on XCD b % 8) owns the row groups
-    // [x nRGx, (x+1) nRGx) and runs every (chunk, segment) unit on them, longest chunks
-    // first; so an XCD's L2 holds only its rows of the images, and the halo rows a
-    // wave re-reads from its neighbour row groups' gradient are read on the same XCD.
-    const int64_t hb = blockIdx.x, xi = hb / 8, x = hb % 8;
-    const int nRGx = (a.nRG + 7) / 8;
-    const int64_t unit = xi / nRGx;
-    const int rg = (int)(x * nRGx + xi % nRGx);
-    if (rg >= a.nRG || unit >= (int64_t)a.nChunk * a.nsegMax) return;
-    const int j = chunk_of_rank((int)(unit / a.nsegMax), a.nChunk, a.jc);
-    const int sg = (int)(unit % a.nsegMax);
-    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
-    __shared__ __attribute__((aligned(16))) float cbuf[FB][48];
-    __shared__ __attribute__((aligned(16))) float pbuf[FB][48];
-    bwd_sweep_body<K>(g, a, j, sg, rg, cbuf, pbuf);
-}
-
 // ---------------------------------------------------------------------------------------
-// Cooperative column sweep (default).  Same decomposition, partial layout and arithmetic
-// as k_bwd_sweep, but one WORKGROUP of 4 waves owns a (chunk, segment, row group) unit:
-// wave v owns rows y0 + 4v .. y0 + 4v + 3.  Per step every gradient element of the unit's
-// 16 + 2r rows is loaded and turned into A = g / S exactly once (own rows by their owner,
-// the 2r halo rows spread over the waves) and published in a double-buffered LDS row
-// array; after one barrier each wave forms the vertical k-row sums V of its own rows and
-// slides them horizontally with a k-deep LDS ring of its own V (HV += V(w) - V(w-k)).  So
-// the leaving column is never re-read (k_bwd_sweep re-reads it: ~1/3 of its HBM traffic)
-// and no halo row is loaded twice (the halo rows miss L2 in k_bwd_sweep), and the leaving
-// column's Y is not needed at all.
-constexpr int NWC = 4;          // waves per cooperative workgroup
-constexpr int TRW = TRB / NWC;  // own rows per wave
+// Cooperative column sweep.  One WORKGROUP of NWC waves owns a (chunk, segment, row group)
+// unit of TRB rows: wave v owns rows y0 + 4v .. y0 + 4v + 3.  Per step every gradient
+// element of the unit's TRB + 2r rows is loaded and turned into A = g / S exactly once
+// (own rows by their owner, the 2r halo rows spread over the waves) and published in a
+// double-buffered LDS row array; after one barrier each wave forms the vertical k-row sums
+// V of its own rows and slides them horizontally with a k-deep LDS ring of its own V
+// (HV += V(w) - V(w-k)).  So the leaving column is never re-read, no halo row is loaded
+// twice within a unit, and the leaving column's Y is not needed at all.  Taller units
+// (CUSTMA_BWD_ROWS = 32: 8 waves) re-read fewer halo rows of the gradient: (TRB + 2r) / TRB
+// gradient reads per voxel.
+constexpr int TRW = 4;           // own rows per wave
+constexpr int NWC = TRB / TRW;   // waves per cooperative workgroup
 #ifndef CUSTMA_BWD_DEPTH
 #define CUSTMA_BWD_DEPTH 1  // 2 measured no faster (C2 full 5.37 vs 5.19 ms): latency is not the limit
 #endif
 constexpr int BDP = CUSTMA_BWD_DEPTH;  // steps of loads in flight (1 or 2)
 #ifndef CUSTMA_BWD_ORDER
-#define CUSTMA_BWD_ORDER 1
+#define CUSTMA_BWD_ORDER 2
 #endif
 #ifndef CUSTMA_BWD_SLIDE
 #define CUSTMA_BWD_SLIDE 1
@@ -483,7 +197,8 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
                                               float* ring, float (*cbuf)[12], float (*pbuf)[12]) {
     constexpr int R = K / 2, NY = TRB + 2 * R, NH = 2 * R;  // NH halo rows
     constexpr int HPW = (NH + NWC - 1) / NWC;                // halo rows per wave (at most)
-    static_assert(NY <= 32, "two row-replicated registers cover the rows");
+    constexpr int NXR = (NY + 15) / 16;  // row-replicated registers holding X of the NY rows
+    static_assert(NXR <= 3, "three row-replicated registers cover the rows");
 
     const ChunkGeo cg = chunk_geo(g, a.dlo, j);
     const int lane = threadIdx.x & 63;
@@ -608,7 +323,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     const i32x4 dY = make_rsrc_sgpr(a.Yp, ib), dM = make_rsrc_sgpr(a.mpp, ib), dP = make_rsrc_sgpr(a.pp, ib);
     const i32x4 dX = make_rsrc_sgpr(a.Xc, ib), dMc = make_rsrc_sgpr(a.mcc, ib), dCc = make_rsrc_sgpr(a.cc, ib);
     struct Ld {
-        uint32_t ge[TRW], cv[TRW], Ye[TRW], mp[TRW], pq[TRW], hg[HP], hY[HP], x0, x1, mc, cx;
+        uint32_t ge[TRW], cv[TRW], Ye[TRW], mp[TRW], pq[TRW], hg[HP], hY[HP], xr[NXR], mc, cx;
     };
     auto issue = [&](int w, Ld& b) {
         const int xb = w - R;
@@ -632,9 +347,10 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             }
         }
         const int r16 = lane & 15;
-        asm_ld4(b.x0, b.x1, b.mc, b.cx, r16 < NY ? img_off((int)ir0 + r16, w) : kOOB,
+        asm_ld4(b.xr[0], b.xr[1], b.mc, b.cx, r16 < NY ? img_off((int)ir0 + r16, w) : kOOB,
                 16 + r16 < NY ? img_off((int)ir0 + 16 + r16, w) : kOOB, img_off(y0i + yw + (lane & 3), w),
                 img_off(y0i + yw + (lane & 3), xb), dX, dMc, dCc);
+        if constexpr (NXR > 2) asm_ld1s(b.xr[2], 32 + r16 < NY ? img_off((int)ir0 + 32 + r16, w) : kOOB, dX, 0u);
     };
     // SLIDE: the current step's projector-side columns (lane l: column w + dl, p': w - R + dl)
     // and the once-per-64-steps column block whose lane i feeds lane 63 at step w0 + 1 + 64k + i
@@ -674,14 +390,16 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             asm_tie(b.hg[i]);
             if constexpr (!SLIDE) asm_tie(b.hY[i]);
         }
-        asm_tie(b.x0); asm_tie(b.x1); asm_tie(b.mc); asm_tie(b.cx);
+#pragma unroll
+        for (int i = 0; i < NXR; ++i) asm_tie(b.xr[i]);
+        asm_tie(b.mc); asm_tie(b.cx);
         if constexpr (SLIDE) tie_cols();
     };
     auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
 
     int sidx = 0;  // ring slot of the current step (step count mod K)
     // loads per issue() (asm_ld5s / asm_ld2s / asm_ld4) and stores per flush(), per thread
-    constexpr int NL = (SLIDE ? TRW * 2 + HP : TRW * 5 + HP * 2) + 4, SF = 6;
+    constexpr int NL = (SLIDE ? TRW * 2 + HP : TRW * 5 + HP * 2) + 4 + (NXR > 2 ? 1 : 0), SF = 6;
     static_assert(NL + SF <= 63, "vmcnt holds the pipeline");
     // cur was issued BDP steps ago; issued since: the later steps' loads, and a flush's SF
     // stores after step s = FBC-1 of the previous block (flush() itself waits until only
@@ -722,10 +440,16 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         const float mco = F(cur.mc) * af;
         const float cxo = (F(cur.cx) - cb) * tf;
         // X of unit row y (wave-uniform y): the lane of the row-replicated register that holds it
+        // (y is wave-uniform but not a compile-time constant: select, never index the register
+        // array dynamically -- that would spill it to scratch at the asm load's issue point)
         auto xrow = [&](int y) -> float {
-            const float x0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)cur.x0, y & 15));
-            const float x1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)cur.x1, y & 15));
-            return y >= 16 ? x1 : x0;
+            float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)cur.xr[0], y & 15));
+#pragma unroll
+            for (int i = 1; i < NXR; ++i) {
+                const float u = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)cur.xr[i], y & 15));
+                v = (y >> 4) == i ? u : v;
+            }
+            return v;
         };
         // ---- own rows: A, and the per-voxel terms (unit rows R + yw .. R + yw + 3) ----
         float amv[TRW], bv[TRW];
@@ -823,22 +547,33 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 template <int K>
 __global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
     // XCD x owns row groups [x nRGx, (x+1) nRGx) (their halo rows are read on one XCD).
-    // CUSTMA_BWD_ORDER 1 (default): units segment-major, chunk rank minor, so the workgroups
-    // resident on an XCD at once hold adjacent diagonal chunks of one column segment: a wave's
-    // 256-byte gradient / volume row segment spans three 128-byte lines whose outer parts the
-    // neighbouring chunk's workgroup reads at the same step (L2 hits instead of a second fetch).
-    // 0: chunk-major (k_bwd_sweep's order).
+    // A wave's 256-byte gradient / volume row segment spans three 128-byte lines whose outer
+    // parts the neighbouring diagonal chunk's workgroup reads at the same step; the order
+    // decides whether those reads meet in the XCD's L2.
+    // CUSTMA_BWD_ORDER 2 (default): on an XCD, chunk rank fastest, then row group, then
+    //   segment -- the chunks of one (row group, segment) are dispatched together.
+    // 1: row group fastest, then chunk rank, then segment.  0: row group, segment, chunk.
     const int64_t hb = blockIdx.x, xi = hb / 8, x = hb % 8;
     const int nRGx = (a.nRG + 7) / 8;
+#if CUSTMA_BWD_ORDER == 2
+    const int jr = (int)(xi % a.nChunk);
+    const int64_t rest = xi / a.nChunk;
+    const int rg = (int)(x * nRGx + rest % nRGx);
+    const int64_t sg64 = rest / nRGx;
+    if (rg >= a.nRG || sg64 >= a.nsegMax) return;
+    const int j = chunk_of_rank(jr, a.nChunk, a.jc);
+    const int sg = (int)sg64;
+#else
     const int64_t unit = xi / nRGx;
     const int rg = (int)(x * nRGx + xi % nRGx);
     if (rg >= a.nRG || unit >= (int64_t)a.nChunk * a.nsegMax) return;
-#if CUSTMA_BWD_ORDER
+#if CUSTMA_BWD_ORDER == 1
     const int j = chunk_of_rank((int)(unit % a.nChunk), a.nChunk, a.jc);
     const int sg = (int)(unit / a.nChunk);
 #else
     const int j = chunk_of_rank((int)(unit / a.nsegMax), a.nChunk, a.jc);
     const int sg = (int)(unit % a.nsegMax);
+#endif
 #endif
     if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
     constexpr int NY = TRB + 2 * (K / 2);
@@ -1032,22 +767,97 @@ __global__ __launch_bounds__(256) void k_bwd_prep(Geo g, const T* __restrict__ c
     prep[5 * plane + p] = to_f(proj[p]);
 }
 
+// ---- the remainder diagonal D of a window layout with D = 64 n (BwdPlan::rem) ----
+// Its voxels (h, w, D) are the last element of every 1028-byte volume row; one strided pass
+// reads them (L2-line granular, ~1/32 of their lines is used, but they are 1/(D+1) of the
+// volume) instead of a fifth chunk of full sweeps with 1 live lane in 64.  Same arithmetic
+// as k_bwd_coop (fp32 A and V, shifted images), added into the gathered sums (fp64):
+//   camera (h, w):  Am += A mp'(h, w+D),  B += V Y(h, w+D),  m'B += V Y mc'(h, w)
+//   projector (h, o = w+D):  Ac += A mc'(h, w),  Bp += V X(h, w),  m'Bp += V X mp'(h, o)
+//   T1c(y, x) += p'(y, x+D) BoxA_D(y, x),  T1p(y, x+D) += c'(y, x) BoxA_D(y, x)
+__global__ __launch_bounds__(256) void k_bwd_rem_voxel(Geo g, BwdArgs a, double* acc, float* remA) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= g.HV() * g.WO) return;
+    const int64_t hv = t / g.WO, w = t % g.WO, h = g.h_lo + hv, D = g.D;
+    const int64_t plane = g.H * g.W, pc = h * g.W + w, po = pc + D;
+    const int64_t e = t * g.DO + D;
+    const float X = a.Xc[pc], Y = a.Yp[po];
+    const float rS = __builtin_amdgcn_rsqf(__builtin_fmaf(X, Y, kEps));
+    const float A = a.grad[e] * rS;
+    const float V = A * a.vol[e] * rS;
+    remA[t] = A;
+    double* c = acc;
+    double* q = acc + 4 * plane;
+    const double vy = (double)(V * Y), vx = (double)(V * X);
+    c[plane + pc] += (double)(A * a.mpp[po]);
+    c[2 * plane + pc] += vy;
+    c[3 * plane + pc] += vy * (double)a.mcc[pc];
+    q[plane + po] += (double)(A * a.mcc[pc]);
+    q[2 * plane + po] += vx;
+    q[3 * plane + po] += vx * (double)a.mpp[po];
+}
+// vertical box of A_D: VA[y - ylo][w] = sum over volume rows h in [y - r, y + r]
+__global__ __launch_bounds__(256) void k_bwd_rem_vbox(Geo g, BwdArgs a, const float* remA, double* remV) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (a.yhi - a.ylo) * g.WO) return;
+    const int64_t y = a.ylo + t / g.WO, w = t % g.WO;
+    int64_t h0 = y - g.r, h1 = y + g.r;
+    h0 = h0 > g.h_lo ? h0 : g.h_lo;
+    h1 = h1 < g.h_hi - 1 ? h1 : g.h_hi - 1;
+    double v = 0.0;
+    for (int64_t h = h0; h <= h1; ++h) v += (double)remA[(h - g.h_lo) * g.WO + w];
+    remV[t] = v;
+}
+// horizontal box and the T1 terms, camera column x in [-r, W) (x < 0: zero padding, c' = -cbar)
+__global__ __launch_bounds__(256) void k_bwd_rem_t1(Geo g, BwdArgs a, const double* remV, double* acc) {
+    const int64_t nx = g.W + g.r;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (a.yhi - a.ylo) * nx) return;
+    const int64_t yy = t / nx, x = t % nx - g.r, y = a.ylo + yy, D = g.D;
+    int64_t w0 = x - g.r, w1 = x + g.r;
+    w0 = w0 > 0 ? w0 : 0;
+    w1 = w1 < g.WO - 1 ? w1 : g.WO - 1;
+    double box = 0.0;
+    for (int64_t w = w0; w <= w1; ++w) box += remV[yy * g.WO + w];
+    const int64_t plane = g.H * g.W;
+    const float cb = a.shift[0], pb = a.shift[1];
+    if (x >= 0) {  // camera pixel (y, x): p'(y, x + D), zero padded past the right edge
+        const float pv = x + D < g.W ? a.pp[y * g.W + x + D] : 0.f;
+        acc[y * g.W + x] += (double)(pv - pb) * box;
+    }
+    if (x + D >= 0 && x + D < g.W) {  // projector pixel (y, x + D)
+        const float cv = x >= 0 ? a.cc[y * g.W + x] : 0.f;
+        acc[4 * plane + y * g.W + x + D] += (double)(cv - cb) * box;
+    }
+}
+
 constexpr int kSumBlocks = 512;
+
+inline size_t a256(size_t n) { return (n + 255) & ~(size_t)255; }
 
 struct BwdPlan {
     int nChunk, S, Sj, nRG, jc, nsegMax;
     bool ok;
     int64_t dlo, ylo, yhi;
-    size_t part_bytes, acc_bytes, cover_bytes, prep_bytes, misc_bytes;
+    bool rem;  // window, D = 64 n: diagonal D handled by k_bwd_rem_* (not a chunk)
+    size_t part_bytes, acc_bytes, cover_bytes, prep_bytes, misc_bytes, rem_bytes;
 };
 
 BwdPlan plan_bwd(const Geo& g) {
     BwdPlan p;
     const int r = g.r;
+    p.rem = false;
     if (g.layout == CUSTMA_LAYOUT_WINDOW) {
         p.dlo = 0;
         p.nChunk = (int)cdiv((int64_t)g.D + 1, NLB);
         p.jc = 0;
+        // D = 64 n: the last diagonal alone would take a fifth chunk of sweeps with one live lane
+        // in 64; k_bwd_rem_* add it instead (one strided pass over it, after k_bwd_gather)
+        const char* er = getenv("CUSTMA_BWD_NOREM");  // benchmarking only
+        if (g.D >= NLB && (g.D + 1) % NLB == 1 && !(er && atoi(er) != 0)) {
+            p.rem = true;
+            p.nChunk -= 1;
+        }
     } else {
         p.dlo = -(g.W - 1);
         p.nChunk = (int)cdiv(2 * g.W - 1, NLB);
@@ -1100,10 +910,11 @@ BwdPlan plan_bwd(const Geo& g) {
     p.cover_bytes = 3 * (size_t)g.W * sizeof(int) + 3 * (size_t)g.W * p.S * sizeof(unsigned short);
     p.prep_bytes = 6 * plane * sizeof(float);
     p.misc_bytes = 2 * kSumBlocks * sizeof(double) + 256;
+    // A of diagonal D [HV][WO] (fp32) and its vertical box [yhi - ylo][WO] (fp64)
+    p.rem_bytes = p.rem ? a256((size_t)g.HV() * g.WO * 4) + (size_t)(p.yhi - p.ylo) * g.WO * 8 : 0;
     return p;
 }
 
-inline size_t a256(size_t n) { return (n + 255) & ~(size_t)255; }
 
 template <typename T>
 hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp,
@@ -1138,16 +949,10 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     const int64_t units = (int64_t)p.nChunk * p.nsegMax * p.nRG;
     const unsigned blocks = (unsigned)(8 * (int64_t)p.nChunk * p.nsegMax * cdiv(p.nRG, 8));
     if (units > 0) {
-        // CUSTMA_BWD_OLD=1: the one-wave-per-unit sweep (re-reads the leaving column), for comparison
-        const char* eo = getenv("CUSTMA_BWD_OLD");
-        const bool old = eo && atoi(eo) != 0;
         prof_begin(PROF_BWD, s);
         switch (g.k) {
 #define CUSTMA_K(KK)                                                                              \
-    case KK:                                                                                      \
-        if (old) hipLaunchKernelGGL((k_bwd_sweep<KK>), dim3(blocks), dim3(64), 0, s, g, a);        \
-        else hipLaunchKernelGGL((k_bwd_coop<KK>), dim3(blocks), dim3(64 * NWC), 0, s, g, a);      \
-        break;
+    case KK: hipLaunchKernelGGL((k_bwd_coop<KK>), dim3(blocks), dim3(64 * NWC), 0, s, g, a); break;
             CUSTMA_SWEEP_KS(CUSTMA_K)
 #undef CUSTMA_K
             default: return hipErrorInvalidValue;
@@ -1156,6 +961,17 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc);
+    if (p.rem) {
+        char* rw = (char*)bsum + a256(p.misc_bytes);  // the plan's rem_bytes follow misc_bytes
+        float* remA = (float*)rw;
+        double* remV = (double*)(rw + a256((size_t)g.HV() * g.WO * 4));
+        hipLaunchKernelGGL(k_bwd_rem_voxel, dim3((unsigned)cdiv(g.HV() * g.WO, 256)), dim3(256), 0, s, g, a, acc,
+                           remA);
+        hipLaunchKernelGGL(k_bwd_rem_vbox, dim3((unsigned)cdiv((p.yhi - p.ylo) * g.WO, 256)), dim3(256), 0, s, g, a,
+                           remA, remV);
+        hipLaunchKernelGGL(k_bwd_rem_t1, dim3((unsigned)cdiv((p.yhi - p.ylo) * (g.W + g.r), 256)), dim3(256), 0, s,
+                           g, a, remV, acc);
+    }
     const int L = 16 + 2 * g.r;
     hipLaunchKernelGGL(k_bwd_combine2<T>, dim3((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2), dim3(256),
                        sizeof(double) * 3 * (L * L + L * 16), s, g, cam, proj, shift, acc, dcam, dproj);
@@ -1166,7 +982,8 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
 
 size_t backward_workspace_bytes(const Geo& g) {
     const BwdPlan p = plan_bwd(g);
-    return a256(p.part_bytes) + a256(p.acc_bytes) + a256(p.cover_bytes) + a256(p.prep_bytes) + a256(p.misc_bytes);
+    return a256(p.part_bytes) + a256(p.acc_bytes) + a256(p.cover_bytes) + a256(p.prep_bytes) + a256(p.misc_bytes) +
+           a256(p.rem_bytes);
 }
 
 bool backward_supported(const Geo& g) {

@@ -1,20 +1,27 @@
-"""Build ablation variants of the HIP library into scripts/_abl/<name>/ (git-ignored)."""
-import os, sys
+"""Build benchmarking variants of the HIP library into scripts/_abl/<name>/ (git-ignored);
+load one with CUSTMA_LIB=scripts/_abl/<name>/libcustma_hip.so.
+Usage: python scripts/build_ablations.py <name> [...]"""
+import os
+import sys
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from custereomatching_amd.build import build_variant
+from custereomatching_amd.build import build_variant  # noqa: E402
+
 HERE = os.path.dirname(os.path.abspath(__file__))
-VARIANTS = {"nostore": ["CUSTMA_ABL_NOSTORE"], "noupdate": ["CUSTMA_ABL_NOUPDATE"],
-            "nothing": ["CUSTMA_ABL_NOSTORE", "CUSTMA_ABL_NOUPDATE"],
-            "storeonly": ["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT"], "skeleton": ["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT", "CUSTMA_ABL_NOSTORE"],
-            "aux1": ["CUSTMA_STORE_AUX=1"], "aux2": ["CUSTMA_STORE_AUX=2"], "aux16": ["CUSTMA_STORE_AUX=16"],
-            "aux3": ["CUSTMA_STORE_AUX=3"], "aux17": ["CUSTMA_STORE_AUX=17"], "aux18": ["CUSTMA_STORE_AUX=18"],
-            "aux19": ["CUSTMA_STORE_AUX=19"],
-            "nowait": ["CUSTMA_ABL_NOWAIT"], "so_nowait": ["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT", "CUSTMA_ABL_NOWAIT"],
-            "tilep2": ["CUSTMA_TILE_P=2"], "border0": ["CUSTMA_BWD_ORDER=0"], "stats7": ["CUSTMA_ABL_STATS7"],
-            "so_stats7": ["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT", "CUSTMA_ABL_STATS7"],
-            "bnoleave": ["CUSTMA_ABL_NOLEAVE"], "bnoimg": ["CUSTMA_ABL_NOIMG"], "bnored": ["CUSTMA_ABL_NORED"],
-            "pf4": ["CUSTMA_BWD_PF=4"], "pf8": ["CUSTMA_BWD_PF=8"], "pf16": ["CUSTMA_BWD_PF=16"],
-            "pf8noall": ["CUSTMA_BWD_PF=8", "CUSTMA_ABL_NOLEAVE", "CUSTMA_ABL_NOIMG", "CUSTMA_ABL_NORED"],
-            "bnoall": ["CUSTMA_ABL_NOLEAVE", "CUSTMA_ABL_NOIMG", "CUSTMA_ABL_NORED"]}
+FWD = ["sweep_wave.hip", "sweep_fwd.hip"]
+BWD = ["bwd_fused.hip"]
+# name: (defines, translation units they affect)
+VARIANTS = {
+    # forward ablations (sweep_wave.hip / sweep_fwd.hip)
+    "nostore": (["CUSTMA_ABL_NOSTORE"], FWD), "noupdate": (["CUSTMA_ABL_NOUPDATE"], FWD),
+    "storeonly": (["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT"], FWD),
+    "nowait": (["CUSTMA_ABL_NOWAIT"], FWD), "stats7": (["CUSTMA_ABL_STATS7"], FWD),
+    # backward unit height / block order (bwd_fused.hip)
+    "r16o1": (["CUSTMA_BWD_ROWS=16", "CUSTMA_BWD_ORDER=1"], BWD),
+    "r16o2": (["CUSTMA_BWD_ROWS=16", "CUSTMA_BWD_ORDER=2"], BWD),
+    "r32o1": (["CUSTMA_BWD_ROWS=32", "CUSTMA_BWD_ORDER=1"], BWD),
+    "r32o2": (["CUSTMA_BWD_ROWS=32", "CUSTMA_BWD_ORDER=2"], BWD),
+}
 for n in (sys.argv[1:] or VARIANTS):
-    print(build_variant(os.path.join(HERE, "_abl", n), VARIANTS[n]))
+    d, only = VARIANTS[n]
+    print(build_variant(os.path.join(HERE, "_abl", n), d, only))

@@ -11,6 +11,7 @@ CFGS = {
     "c2_win": dict(H=1024, W=1024, k=9, D=128, layout="window", dtype=torch.float32),
     "c3_win": dict(H=2048, W=2048, k=11, D=256, layout="window", dtype=torch.float16),
     "c3_full": dict(H=2048, W=2048, k=11, D=256, layout="full", dtype=torch.float16),
+    "c5_win": dict(H=4096, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
 }
 
 def run(name, ops, reps):

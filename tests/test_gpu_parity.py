@@ -217,6 +217,10 @@ BWD_CASES = [
     # many steps per segment: several flush blocks of the backward's load pipeline
     (36, 200, 11, 60, "textured"),
     (34, 260, 9, 100, "smooth"),
+    # window D = 64 n: the last diagonal goes through the remainder kernels (k_bwd_rem_*)
+    (20, 100, 5, 64, "textured"),
+    (18, 300, 11, 256, "smooth"),
+    (16, 140, 15, 128, "quantized"),
     # generic fp64 backward (no fused instantiation): odd k > 15 and even k
     (20, 44, 17, 9, "textured"),
     (16, 40, 25, 12, "smooth"),
