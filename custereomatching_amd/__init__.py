@@ -7,7 +7,8 @@ hand-written HIP kernels behind the C ABI of include/custma.h.
 """
 from .version import __version__
 from .stereo_matching_wrapper import stereo_matching, cost_volume_forward, cost_volume_backward, default_precision
-from .disparity import (stereo_disparity, volume_argmax, disparity_from_index, confidence_mask, soft_argmax)
+from .disparity import (stereo_disparity, stereo_disparity_soft, disparity_maps, volume_argmax, disparity_from_index,
+                        confidence_mask, soft_argmax)
 from .preprocess import image_u8_to_unit
 from .utils import Timer, TimerError
 

@@ -23,7 +23,7 @@ E_ARG, E_NULL, E_WORKSPACE, E_LAUNCH, E_UNSUPPORTED = -1, -2, -3, -4, -5
 EXPORTS = ("custma_abi_version", "custma_last_error", "custma_volume_dims", "custma_workspace_bytes",
            "custma_forward", "custma_backward", "custma_argmax", "custma_disparity", "custma_forward_band",
            "custma_backward_band", "custma_disparity_band", "custma_profile_enable", "custma_profile_mean_ms",
-           "custma_image_u8_to_unit")
+           "custma_image_u8_to_unit", "custma_disparity_soft_band")
 
 
 class CustmaError(RuntimeError):
@@ -52,12 +52,15 @@ def _load():
                                          vp]
     lib.custma_disparity_band.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, vp, vp, vp, vp, sz,
                                           vp]
+    f32 = ctypes.c_float
+    lib.custma_disparity_soft_band.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, f32, f32, vp, vp, vp,
+                                               vp, vp, vp, sz, vp]
     lib.custma_profile_enable.argtypes = [i32]
     lib.custma_image_u8_to_unit.argtypes = [vp, i64, i64, i32, i32, i32, vp, vp]
     lib.custma_profile_mean_ms.argtypes = [i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int32)]
     for name in ("custma_profile_enable", "custma_profile_mean_ms", "custma_forward", "custma_backward", "custma_argmax", "custma_disparity",
                  "custma_volume_dims", "custma_forward_band", "custma_backward_band", "custma_disparity_band",
-                 "custma_image_u8_to_unit"):
+                 "custma_image_u8_to_unit", "custma_disparity_soft_band"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
 

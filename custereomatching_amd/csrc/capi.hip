@@ -321,8 +321,30 @@ int custma_disparity_band(const void* camera, const void* projector, int32_t dty
     Stats sc, sp;
     if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
     void* ws2 = (char*)workspace + stats_bytes(g);
-    return check_hip(launch_disparity(camera, projector, dtype, g, sc, sp, index, best, n_rechecked, ws2, s),
+    return check_hip(launch_disparity(camera, projector, dtype, g, sc, sp, index, best, n_rechecked, ws2, s, nullptr,
+                                      0.f, nullptr, 0.f),
                      "disparity");
+}
+
+int custma_disparity_soft_band(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                               int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin, int64_t row_end,
+                               float beta, float threshold, int64_t* index, float* best, float* soft, float* mask,
+                               int32_t* n_rechecked, void* workspace, size_t workspace_bytes, void* stream) {
+    Geo g;
+    int rc = make_geo(H, W, kernel_size, layout, D, &g);
+    if (rc || (rc = check_dtype(dtype)) || (rc = set_band(&g, row_begin, row_end))) return rc;
+    if (soft && !(beta > 0.f)) return fail(CUSTMA_E_ARG, "soft-argmax needs beta > 0, got %g", (double)beta);
+    if (g.HV() == 0 || g.W == 0) return CUSTMA_OK;
+    if (!camera || !projector || !index || !workspace) return fail(CUSTMA_E_NULL, "null pointer argument");
+    if (workspace_bytes < stats_bytes(g) + align256(disparity_partial_bytes(g)))
+        return fail(CUSTMA_E_WORKSPACE, "workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    Stats sc, sp;
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
+    void* ws2 = (char*)workspace + stats_bytes(g);
+    return check_hip(launch_disparity(camera, projector, dtype, g, sc, sp, index, best, n_rechecked, ws2, s, soft,
+                                      beta, mask, threshold),
+                     "disparity_soft");
 }
 
 }  // extern "C"

@@ -241,8 +241,10 @@ hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const G
                            float* out, hipStream_t s);
 hipError_t launch_argmax(const float* vol, int64_t rows, int64_t n, int64_t* idx, float* best, hipStream_t s);
 size_t disparity_partial_bytes(const Geo& g);
+// soft (nullable): soft-argmax with beta; mask (nullable): best > threshold as 1 / 0
 hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
-                            int64_t* idx, float* best, int32_t* n_rechecked, void* ws, hipStream_t s);
+                            int64_t* idx, float* best, int32_t* n_rechecked, void* ws, hipStream_t s, float* soft,
+                            float beta, float* mask, float threshold);
 size_t backward_workspace_bytes(const Geo& g);
 bool backward_supported(const Geo& g);
 // generic backward (any k; bwd_generic.hip)

@@ -96,21 +96,32 @@ __device__ __forceinline__ int64_t d_of_s(const Geo& g, int64_t w, int64_t s) {
     return g.layout == CUSTMA_LAYOUT_WINDOW ? w + s : s;
 }
 
+// Optional outputs of the fused disparity beyond (index, best): soft-argmax with beta
+// (examples/verify.py:31-39) and the max-cost confidence mask (verify.py:72-74).
+struct SoftOut {
+    float* soft;  // [HV][WO] or null
+    float* mask;  // [HV][WO] or null: 1 where best > threshold, else 0
+    float kb;     // beta * log2(e)
+    float threshold;
+};
+
 template <typename T, int KT>
 __global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                     Stats sc, Stats sp, DispPartial part, int nChunk, float tau,
                                                     int64_t* __restrict__ idx, float* __restrict__ best,
-                                                    int32_t* __restrict__ counter, int64_t* __restrict__ queue) {
+                                                    int32_t* __restrict__ counter, int64_t* __restrict__ queue,
+                                                    SoftOut so) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t npix = g.HV() * g.WO;
     if (p >= npix) return;
-    float b = -FLT_MAX, sec = -FLT_MAX;
+    float b = -FLT_MAX, sec = -FLT_MAX, q0 = 0.f, q1 = 0.f;
     int64_t bi = INT64_MAX;
     for (int c = 0; c < nChunk; ++c) {
         const int64_t q = (int64_t)c * npix + p;
         const int32_t oi = part.index[q];
         if (oi < 0) continue;
         const float ob = part.best[q], os = part.second[q];
+        if (so.soft) soft_merge(b, ob, part.s0[q], part.s1[q], so.kb, q0, q1);
         if (ob > b || (ob == b && oi < bi)) {
             sec = fmaxf(os, b); b = ob; bi = oi;
         } else {
@@ -120,7 +131,10 @@ __global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, c
     const int64_t h = g.h_lo + p / g.WO, w = p % g.WO;
     if (bi != INT64_MAX && (sec == -FLT_MAX || b - sec > tau)) {
         idx[p] = bi;
-        if (best) best[p] = exact_cost<T, KT>(cam, proj, g, sc, sp, h, w, d_of_s(g, w, bi));
+        const float eb = exact_cost<T, KT>(cam, proj, g, sc, sp, h, w, d_of_s(g, w, bi));
+        if (best) best[p] = eb;
+        if (so.mask) so.mask[p] = eb > so.threshold ? 1.f : 0.f;
+        if (so.soft) so.soft[p] = q1 / q0;
     } else {
         const int32_t slot = atomicAdd(counter, 1);
         queue[slot] = p;
@@ -131,34 +145,44 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_disp_recheck(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                       Stats sc, Stats sp, const int32_t* __restrict__ counter,
                                                       const int64_t* __restrict__ queue, int64_t* __restrict__ idx,
-                                                      float* __restrict__ best) {
-    __shared__ float rv[4];
+                                                      float* __restrict__ best, SoftOut so) {
+    __shared__ float rv[4], r0[4], r1[4];
     __shared__ int64_t ri[4];
     const int n = *counter;
     for (int64_t e = blockIdx.x; e < n; e += gridDim.x) {
         const int64_t p = queue[e];
         const int64_t h = g.h_lo + p / g.WO, w = p % g.WO;
-        float bv = -INFINITY;
+        float bv = -INFINITY, q0 = 0.f, q1 = 0.f;
         int64_t bi = INT64_MAX;
         for (int64_t s = threadIdx.x; s < g.DO; s += blockDim.x) {
             const int64_t d = d_of_s(g, w, s);
             if (!voxel_valid(g, w, d)) continue;
             const float c = exact_cost(cam, proj, g, sc, sp, h, w, d);
+            if (so.soft) soft_add(c, (float)s, bv, so.kb, q0, q1);
             amax_merge(bv, bi, c, s);
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const float ov = __shfl_xor(bv, off);
             const int64_t oi = __shfl_xor(bi, off);
+            if (so.soft) {
+                const float o0 = __shfl_xor(q0, off), o1 = __shfl_xor(q1, off);
+                soft_merge(bv, ov, o0, o1, so.kb, q0, q1);
+            }
             amax_merge(bv, bi, ov, oi);
         }
         const int wave = threadIdx.x >> 6;
-        if ((threadIdx.x & 63) == 0) { rv[wave] = bv; ri[wave] = bi; }
+        if ((threadIdx.x & 63) == 0) { rv[wave] = bv; ri[wave] = bi; r0[wave] = q0; r1[wave] = q1; }
         __syncthreads();
         if (threadIdx.x == 0) {
-            for (int q = 1; q < (int)(blockDim.x >> 6); ++q) amax_merge(bv, bi, rv[q], ri[q]);
+            for (int q = 1; q < (int)(blockDim.x >> 6); ++q) {
+                if (so.soft) soft_merge(bv, rv[q], r0[q], r1[q], so.kb, q0, q1);
+                amax_merge(bv, bi, rv[q], ri[q]);
+            }
             idx[p] = bi;
             if (best) best[p] = bv;
+            if (so.mask) so.mask[p] = bv > so.threshold ? 1.f : 0.f;
+            if (so.soft) so.soft[p] = q1 / q0;
         }
         __syncthreads();
     }
@@ -176,11 +200,17 @@ hipError_t launch_argmax(const float* vol, int64_t rows, int64_t n, int64_t* idx
 size_t disparity_partial_bytes(const Geo& g) {
     const SweepGrid sg = sweep_grid(g);
     const size_t n = (size_t)sg.nChunk * g.HV() * g.WO;
-    return n * (4 + 4 + 4) + (size_t)g.HV() * g.WO * 8 + 256;
+    return n * (4 + 4 + 4 + 4 + 4) + (size_t)g.HV() * g.WO * 8 + 256;
 }
 
 hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
-                            int64_t* idx, float* best, int32_t* n_rechecked, void* ws, hipStream_t s) {
+                            int64_t* idx, float* best, int32_t* n_rechecked, void* ws, hipStream_t s, float* soft,
+                            float beta, float* mask, float threshold) {
+    SoftOut so;
+    so.soft = soft;
+    so.mask = mask;
+    so.kb = beta * 1.4426950408889634f;
+    so.threshold = threshold;
     const SweepGrid sg = sweep_grid(g);
     const size_t n = (size_t)sg.nChunk * g.HV() * g.WO;
     char* p = (char*)ws;
@@ -192,6 +222,9 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
     part.best = (float*)p;
     part.second = part.best + n;
     part.index = (int32_t*)(part.second + n);
+    part.s0 = soft ? (float*)(part.index + n) : nullptr;
+    part.s1 = soft ? part.s0 + n : nullptr;
+    part.kb = so.kb;
     hipError_t e = hipMemsetAsync(counter, 0, 4, s);
     if (e != hipSuccess) return e;
     // kernel sizes without a sweep instantiation: every pixel is decided exactly
@@ -212,10 +245,10 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
         constexpr int KT = decltype(kc)::value;
         if (dtype == CUSTMA_F16)
             hipLaunchKernelGGL((k_disp_merge<__half, KT>), dim3(mb), dim3(256), 0, s, (const __half*)cam,
-                               (const __half*)proj, g, sc, sp, part, nChunk, tau, idx, best, counter, queue);
+                               (const __half*)proj, g, sc, sp, part, nChunk, tau, idx, best, counter, queue, so);
         else
             hipLaunchKernelGGL((k_disp_merge<float, KT>), dim3(mb), dim3(256), 0, s, (const float*)cam,
-                               (const float*)proj, g, sc, sp, part, nChunk, tau, idx, best, counter, queue);
+                               (const float*)proj, g, sc, sp, part, nChunk, tau, idx, best, counter, queue, so);
     };
     switch (g.k) {
 #define CUSTMA_K(KK) \
@@ -226,10 +259,10 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
     }
     if (dtype == CUSTMA_F16) {
         hipLaunchKernelGGL(k_disp_recheck<__half>, dim3(2048), dim3(256), 0, s, (const __half*)cam,
-                           (const __half*)proj, g, sc, sp, counter, queue, idx, best);
+                           (const __half*)proj, g, sc, sp, counter, queue, idx, best, so);
     } else {
         hipLaunchKernelGGL(k_disp_recheck<float>, dim3(2048), dim3(256), 0, s, (const float*)cam,
-                           (const float*)proj, g, sc, sp, counter, queue, idx, best);
+                           (const float*)proj, g, sc, sp, counter, queue, idx, best, so);
     }
     e = hipGetLastError();
     if (e == hipSuccess && n_rechecked) e = hipMemcpyAsync(n_rechecked, counter, 4, hipMemcpyDeviceToDevice, s);

@@ -101,7 +101,36 @@ struct DispPartial {
     float* best;     // [nChunk][HV][WO]
     float* second;   // [nChunk][HV][WO]
     int32_t* index;  // [nChunk][HV][WO] layout index s of best, -1 if none
+    // soft-argmax (examples/verify.py:31-39): with kb = beta * log2(e) > 0, the chunk's
+    // sum of exp(beta (cost - best)) and of s * exp(beta (cost - best)) (s = layout index)
+    float* s0;       // [nChunk][HV][WO] or null
+    float* s1;       // [nChunk][HV][WO] or null
+    float kb;
 };
+
+// Online soft-argmax accumulation next to the running (best, second, first index): the
+// weights are taken relative to the running best (rescaled when it grows), so they never
+// overflow; invalid entries (-FLT_MAX) carry no weight.
+__device__ __forceinline__ void soft_add(float v, float idx, float best_before, float kb, float& s0, float& s1) {
+    if (v > best_before) {
+        const float sc = __builtin_amdgcn_exp2f(kb * (best_before - v));
+        s0 = s0 * sc + 1.f;
+        s1 = s1 * sc + idx;
+    } else {
+        const float wgt = __builtin_amdgcn_exp2f(kb * (v - best_before));
+        s0 += wgt;
+        s1 += wgt * idx;
+    }
+}
+// merge another accumulator (bo, o0, o1) into (b, s0, s1); both relative to their own best
+__device__ __forceinline__ void soft_merge(float b, float bo, float o0, float o1, float kb, float& s0, float& s1) {
+    const float m = b > bo ? b : bo;
+    // the side holding the max has factor 1 exactly (no inf - inf when both are empty)
+    const float fa = b == m ? 1.f : __builtin_amdgcn_exp2f(kb * (b - m));
+    const float fb = bo == m ? 1.f : __builtin_amdgcn_exp2f(kb * (bo - m));
+    s0 = s0 * fa + o0 * fb;
+    s1 = s1 * fa + o1 * fb;
+}
 
 // Lane / chunk geometry.
 //

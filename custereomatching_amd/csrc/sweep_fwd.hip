@@ -370,18 +370,26 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 const int PER = (NL + TPR - 1) / TPR;
                 const int m = tid / TPR, part_i = tid % TPR;
                 const bool red_live = m < TWT;
-                float best = -FLT_MAX, second = -FLT_MAX;
+                float best = -FLT_MAX, second = -FLT_MAX, q0 = 0.f, q1 = 0.f;
                 int bi = 0x7fffffff;
+                const bool soft = part.s0 != nullptr;
+                // layout index s of diagonal lane l for camera column u0 + m
+                const float sbase = (float)(window ? d0 : u0 + m + d0);
                 for (int e = 0; red_live && e < PER; ++e) {
                     const int l = part_i * PER + e;
                     if (l >= NL) break;
                     const float v = stg[m * NL + l];
+                    if (soft && v > -FLT_MAX) soft_add(v, sbase + (float)l, best, part.kb, q0, q1);
                     if (v > best) { second = best; best = v; bi = l; }
                     else if (v > second) second = v;
                 }
                 for (int off = 1; off < TPR; off <<= 1) {
                     const float ob = __shfl_xor(best, off), os = __shfl_xor(second, off);
                     const int oi = __shfl_xor(bi, off);
+                    if (soft) {
+                        const float o0 = __shfl_xor(q0, off), o1 = __shfl_xor(q1, off);
+                        soft_merge(best, ob, o0, o1, part.kb, q0, q1);
+                    }
                     if (ob > best || (ob == best && oi < bi)) {
                         second = fmaxf(os, best); best = ob; bi = oi;
                     } else {
@@ -399,6 +407,10 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                         sidx = window ? dd : u + dd;
                     }
                     part.index[pidx] = (int32_t)sidx;
+                    if (soft) {
+                        part.s0[pidx] = q0;
+                        part.s1[pidx] = q1;
+                    }
                 }
             }
         }

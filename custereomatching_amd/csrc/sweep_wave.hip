@@ -154,7 +154,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     auto compute = [&](Stage& p, int64_t t) {
         // loads(t) were issued at the end of step t-P; after them, for each step s in
         // t-P+1 .. t-1: its stores (from step h0 on) and loads(s+P)
-        constexpr int ST = AMX > 0 ? 3 * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);  // stores/step
+        constexpr int ST = AMX > 0 ? 5 * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);  // stores/step
         static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
 #ifdef CUSTMA_ABL_NOWAIT  // ablation builds only: no wait for the loads (garbage values)
         asm_vmcnt<63>();
@@ -296,10 +296,15 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                     const uint32_t pb = (uint32_t)(nrow * 4);
                     const auto rB = make_rsrc(part.best + prow, pb), rS = make_rsrc(part.second + prow, pb);
                     const auto rI = make_rsrc(part.index + prow, pb);
+                    // soft-argmax sums (null arrays: out-of-range stores, so the store count holds)
+                    const bool soft = part.s0 != nullptr;
+                    const auto rQ0 = make_rsrc(soft ? part.s0 + prow : part.best, soft ? pb : 0u);
+                    const auto rQ1 = make_rsrc(soft ? part.s1 + prow : part.best, soft ? pb : 0u);
+                    const float kb = part.kb;
 #pragma unroll
                     for (int ps = 0; ps < AMX; ++ps) {
                         const int m = (ps * nw + wv) * 4 + (l >> 4);  // tile row of this 16-lane group
-                        float b = -FLT_MAX, sec = -FLT_MAX;
+                        float b = -FLT_MAX, sec = -FLT_MAX, q0 = 0.f, q1 = 0.f;
                         int bi = INT_MAX;
                         // increasing s per lane: the first index wins among equal values
                         const int mr = m < TW ? m : 0;
@@ -308,6 +313,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                             const int s2 = sub + 16 * i;
                             if (s2 < (int)DO) {
                                 const float v = sb[mr * DO + s2];
+                                if (soft) soft_add(v, (float)s2, b, kb, q0, q1);
                                 const bool gt = v > b;
                                 sec = gt ? b : fmaxf(sec, v);
                                 bi = gt ? s2 : bi;
@@ -318,6 +324,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                         for (int off = 8; off > 0; off >>= 1) {
                             const float ob = __shfl_xor(b, off), os = __shfl_xor(sec, off);
                             const int oi = __shfl_xor(bi, off);
+                            if (soft) {
+                                const float o0 = __shfl_xor(q0, off), o1 = __shfl_xor(q1, off);
+                                soft_merge(b, ob, o0, o1, kb, q0, q1);
+                            }
                             if (ob > b || (ob == b && oi < bi)) { sec = fmaxf(os, b); b = ob; bi = oi; }
                             else sec = fmaxf(sec, ob);
                         }
@@ -325,6 +335,9 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, b), rB, vo, 0u, 0);
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, sec), rS, vo, 0u, 0);
                         __builtin_amdgcn_raw_buffer_store_b32((unsigned int)(bi == INT_MAX ? -1 : bi), rI, vo, 0u, 0);
+                        const uint32_t vq = soft ? vo : OOB;
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, q0), rQ0, vq, 0u, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, q1), rQ1, vq, 0u, 0);
                     }
                 } else if constexpr (SS < 0) {  // block base 16-byte aligned (checked at launch)
                     const int n4 = total >> 2;

@@ -6,6 +6,11 @@
   bit-identical to ``argmax`` of the exact (reference-arithmetic) volume:
   pixels whose fast top-2 gap is inside the fast path's error margin are
   re-decided with the exact arithmetic on the GPU.
+* :func:`stereo_disparity_soft` -- the same fused pass also returning the
+  soft-argmax (softmax(beta * cost) . index, verify.py:31-39) and the max-cost
+  confidence mask (verify.py:72-74), still without the volume;
+  :func:`disparity_maps` turns them into the caller's disparity maps
+  (examples/test.py:78-86).
 * :func:`volume_argmax` -- first-index argmax of a materialised volume
   (``torch.max(cost_volume.reshape(H*W, -1), -1)`` at verify.py:72).
 * :func:`disparity_from_index`, :func:`confidence_mask`, :func:`soft_argmax`
@@ -48,6 +53,56 @@ def stereo_disparity(camera: torch.Tensor, projector: torch.Tensor, D: int, kern
     if return_rechecked:
         return idx, best, nre
     return idx, best
+
+
+def stereo_disparity_soft(camera: torch.Tensor, projector: torch.Tensor, D: int, kernel_size: int,
+                          layout: str = "full", beta: float = 50.0, threshold: float = 0.6,
+                          rows: Optional[Tuple[int, int]] = None, return_rechecked: bool = False):
+    """(index int64, best fp32, soft fp32, mask fp32), each [H, WO], from one fused pass
+    (custma_disparity_soft_band): index / best as :func:`stereo_disparity`; soft =
+    sum_s s * softmax(beta * cost)_s over the volume's last axis (verify.py:31-39, the
+    defaults are its beta = 50 and threshold = 0.6, verify.py:12-13); mask = 1 where
+    best > threshold else 0 (verify.py:72-74).  The volume is never materialised."""
+    code = _check_pair(camera, projector, kernel_size)
+    if not beta > 0:
+        raise ValueError(f"beta must be > 0, got {beta}")
+    lay = _LAYOUTS[layout]
+    H, W = camera.shape
+    r0, r1 = _rows(H, rows)
+    Dl = int(D) if lay == _lib.LAYOUT_WINDOW else 0
+    WO, _ = _lib.volume_dims(H, W, lay, Dl)
+    dev = camera.device
+    idx = torch.empty((r1 - r0, WO), dtype=torch.int64, device=dev)
+    best = torch.empty((r1 - r0, WO), dtype=torch.float32, device=dev)
+    soft = torch.empty((r1 - r0, WO), dtype=torch.float32, device=dev)
+    mask = torch.empty((r1 - r0, WO), dtype=torch.float32, device=dev)
+    nre = torch.zeros(1, dtype=torch.int32, device=dev)
+    if idx.numel():
+        with torch.cuda.device(dev):
+            nb = _lib.workspace_bytes(H, W, kernel_size, lay, Dl, _lib.OP_DISPARITY)
+            ws = _workspace(nb, dev)
+            _lib.check(_lib.lib.custma_disparity_soft_band(
+                camera.data_ptr(), projector.data_ptr(), code, H, W, kernel_size, lay, Dl, r0, r1, float(beta),
+                float(threshold), idx.data_ptr(), best.data_ptr(), soft.data_ptr(), mask.data_ptr(), nre.data_ptr(),
+                ws.data_ptr(), ws.numel(), _stream_ptr(dev)), "stereo_disparity_soft")
+    if return_rechecked:
+        return idx, best, soft, mask, nre
+    return idx, best, soft, mask
+
+
+def disparity_maps(camera: torch.Tensor, projector: torch.Tensor, D: int, kernel_size: int, layout: str = "full",
+                   beta: float = 50.0, threshold: float = 0.6):
+    """The reference caller's disparity pipeline (examples/test.py:71-86) from one fused pass:
+    returns (disparity, disparity_softargmax, mask), both disparities multiplied by the mask
+    (test.py:84, 86).  Full layout: template - argmax with template = camera column w
+    (test.py:82-83); window layout: the index s is the offset d - w, so the disparity is -s."""
+    idx, best, soft, mask = stereo_disparity_soft(camera, projector, D, kernel_size, layout, beta, threshold)
+    if layout == "window":
+        disp, disp_soft = -idx.to(torch.float32), -soft
+    else:
+        w = torch.arange(idx.shape[-1], device=idx.device, dtype=torch.float32)
+        disp, disp_soft = w - idx.to(torch.float32), w - soft
+    return disp * mask, disp_soft * mask, mask
 
 
 def volume_argmax(cost_volume: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -136,6 +136,19 @@ int custma_disparity(const void* camera, const void* projector, int32_t dtype, i
                      int32_t kernel_size, int32_t layout, int32_t D, int64_t* index, float* best,
                      int32_t* n_rechecked, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Fused disparity with the rest of the reference caller's post-processing, still without the volume
+ * (examples/test.py:78-86; examples/verify.py:31-39 soft_argmax, :72-74 max-cost mask), over volume rows
+ * [row_begin, row_end) of a (haloed) band:
+ *   index, best   as custma_disparity (index certified bit-identical to argmax of the exact volume)
+ *   soft          (nullable) sum_s s softmax(beta * cost)_s over the layout's last axis s, from the fast
+ *                 costs (the exact ones for re-decided pixels); beta > 0
+ *   mask          (nullable) 1.0f where best > threshold, else 0.0f (the reference's torch.where)
+ * Workspace: custma_workspace_bytes(..., CUSTMA_OP_DISPARITY). */
+int custma_disparity_soft_band(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                               int32_t kernel_size, int32_t layout, int32_t D, int64_t row_begin, int64_t row_end,
+                               float beta, float threshold, int64_t* index, float* best, float* soft, float* mask,
+                               int32_t* n_rechecked, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

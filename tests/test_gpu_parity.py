@@ -422,3 +422,48 @@ def test_backward_wide_full_layout_many_chunks(gpu):
     gc, gp = cm.cost_volume_backward(_dev(g, gpu), _dev(cam, gpu), _dev(proj, gpu), k, projector_grad=True)
     assert np.abs(gc.cpu().numpy() - rc).max() <= 1e-5 * max(1, np.abs(rc).max())
     assert np.abs(gp.cpu().numpy() - rp).max() <= 1e-5 * max(1, np.abs(rp).max())
+
+
+def _soft_argmax_ref(vol, beta):
+    """examples/verify.py:31-39 restated in float64 on the oracle's exact volume."""
+    x = torch.from_numpy(vol).double()
+    p = torch.softmax(x * beta, dim=-1)
+    return (p * torch.arange(x.shape[-1], dtype=torch.float64)).sum(-1).numpy(), p.numpy()
+
+
+SOFT_CASES = [
+    (24, 96, 5, 24, "full"), (24, 96, 9, 40, "window"), (20, 320, 11, 256, "window"),  # tile kernel
+    (18, 200, 7, 150, "window"), (20, 40, 17, 12, "full"), (16, 48, 4, 10, "window"),  # exact-decided
+    (24, 48, 5, 16, "full"),
+]
+
+
+@pytest.mark.parametrize("case", SOFT_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_D{c[3]}_{c[4]}" for c in SOFT_CASES])
+@pytest.mark.parametrize("kind", ["textured", "constant"])
+def test_disparity_soft_argmax_and_mask(gpu, case, kind):
+    """Fused soft-argmax (beta = 50) and max-cost mask (threshold 0.6), examples/verify.py:31-39, 72-74,
+    without the volume.  Index / best / mask bit-identical to the exact volume's; soft within the
+    first-order propagation of the fast path's cost error eps: |d soft| <= 2 beta eps E_w|s - soft|
+    (+ fp32 rounding of the sums, 1e-5 relative)."""
+    H, W, k, D, layout = case
+    beta, thr = 50.0, 0.6
+    cam, proj = make_pair(H, W, D, seed=81, kind=kind)
+    lay, Dl = _layout_args(layout, D)
+    ref = O.forward(cam, proj, k, layout=lay, D=Dl)
+    ridx, rbest = O.argmax(ref)
+    rsoft, pw = _soft_argmax_ref(ref, beta)
+    idx, best, soft, mask = cm.stereo_disparity_soft(_dev(cam, gpu), _dev(proj, gpu), D, k, layout, beta, thr)
+    idx, best, soft, mask = (t.cpu().numpy() for t in (idx, best, soft, mask))
+    assert np.array_equal(idx, ridx)
+    assert np.array_equal(best.view(np.uint32), rbest.view(np.uint32))
+    assert np.array_equal(mask, (rbest > thr).astype(np.float32))
+    s = np.arange(ref.shape[-1], dtype=np.float64)
+    spread = (pw * np.abs(s - rsoft[..., None])).sum(-1)
+    tol = 2.0 * beta * O.fast_tolerance(k) * spread + 1e-5 * np.maximum(1.0, rsoft)
+    err = np.abs(soft - rsoft)
+    assert np.all(err <= tol), float((err / tol).max())
+    # the caller pipeline (examples/test.py:78-86) from the fused pass
+    dmap, dsoft, m2 = cm.disparity_maps(_dev(cam, gpu), _dev(proj, gpu), D, k, layout, beta, thr)
+    w = np.arange(ref.shape[1], dtype=np.float32)
+    want = ((-ridx if layout == "window" else w - ridx) * (rbest > thr)).astype(np.float32)
+    assert np.array_equal(dmap.cpu().numpy(), want)
