@@ -16,6 +16,12 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libcustma_hip.so")
 SOURCES = ["capi.hip", "stats.hip", "fwd_exact.hip", "sweep_fwd.hip", "sweep_wave.hip", "bwd_fused.hip", "bwd_generic.hip", "select.hip", "preprocess.hip"]
+SWEEP_KS = (1, 3, 5, 7, 9, 11, 13, 15)  # CUSTMA_SWEEP_KS in csrc/sweep.h
+# translation units: (object name, source, defines).  sweep_wave.hip compiles once per kernel
+# size (its instantiations dominate the build) plus once for the dispatch.
+UNITS = [(os.path.splitext(src)[0], src, []) for src in SOURCES if src != "sweep_wave.hip"]
+UNITS += [("sweep_wave_d", "sweep_wave.hip", ["-DCUSTMA_SW_DISPATCH"])]
+UNITS += [(f"sweep_wave_k{k}", "sweep_wave.hip", [f"-DCUSTMA_SW_K={k}"]) for k in SWEEP_KS]
 ARCH = os.environ.get("CUSTMA_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: fused multiply-adds only where written (__builtin_fmaf / fma);
@@ -24,8 +30,8 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract
           "-fno-gpu-rdc", "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
 
 
-def _obj(src):
-    return os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
+def _obj(unit, libdir=LIBDIR):
+    return os.path.join(libdir, unit[0] + ".o")
 
 
 def _deps():
@@ -33,12 +39,13 @@ def _deps():
         os.path.join(HERE, "..", "include", "custma.h")]
 
 
-def _compile(src, extra=(), libdir=LIBDIR):
-    out = os.path.join(libdir, os.path.splitext(src)[0] + ".o")
-    cmd = [HIPCC, *CFLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", out]
+def _compile(unit, extra=(), libdir=LIBDIR):
+    name, src, defs = unit
+    out = _obj(unit, libdir)
+    cmd = [HIPCC, *CFLAGS, *defs, *extra, "-c", os.path.join(CSRC, src), "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+        raise RuntimeError(f"hipcc failed for {name} ({src}):\n{r.stderr}")
     return out
 
 
@@ -47,11 +54,11 @@ def _headers():
         os.path.join(HERE, "..", "include", "custma.h")]
 
 
-def _stale(src, hdr_mtime):
-    o = _obj(src)
+def _stale(unit, hdr_mtime):
+    o = _obj(unit)
     if not os.path.exists(o):
         return True
-    return os.path.getmtime(o) < max(hdr_mtime, os.path.getmtime(os.path.join(CSRC, src)))
+    return os.path.getmtime(o) < max(hdr_mtime, os.path.getmtime(os.path.join(CSRC, unit[1])))
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -61,10 +68,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
         return LIB
     hdr = max(os.path.getmtime(p) for p in _headers())
-    todo = [s for s in SOURCES if force or _stale(s, hdr)]
+    todo = [u for u in UNITS if force or _stale(u, hdr)]
     with cf.ThreadPoolExecutor(max_workers=max(1, min(len(todo), os.cpu_count() or 4))) as ex:
         list(ex.map(_compile, todo))
-    objs = [_obj(s) for s in SOURCES]
+    objs = [_obj(u) for u in UNITS]
     cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -80,12 +87,12 @@ def build_variant(libdir: str, defines, only=None) -> str:
     switches affect (the rest link from the main build's objects)."""
     os.makedirs(libdir, exist_ok=True)
     extra = [f"-D{d}" for d in defines]
-    todo = [s for s in SOURCES if only is None or s in only]
+    todo = [u for u in UNITS if only is None or u[1] in only]
     if only is not None:
         build()
     with cf.ThreadPoolExecutor(max_workers=max(1, min(len(todo), os.cpu_count() or 4))) as ex:
-        done = dict(zip(todo, ex.map(lambda s: _compile(s, extra, libdir), todo)))
-    objs = [done.get(s, _obj(s)) for s in SOURCES]
+        done = dict(zip([u[0] for u in todo], ex.map(lambda u: _compile(u, extra, libdir), todo)))
+    objs = [done.get(u[0], _obj(u)) for u in UNITS]
     lib = os.path.join(libdir, "libcustma_hip.so")
     r = subprocess.run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", lib, *objs], capture_output=True, text=True)
     if r.returncode != 0:

@@ -190,6 +190,14 @@ hipError_t launch_fwd_lds(const void* cam, const void* proj, int dtype, const Ge
 
 inline int64_t sweep_blocks(const SweepGrid& sg) { return (int64_t)sg.nBand * sg.nTile * sg.nChunk; }
 
+// per-kernel-size entry points of sweep_wave.hip (one translation unit per size)
+template <int K>
+hipError_t sw_fwd(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, float* out,
+                  hipStream_t s);
+template <int K>
+hipError_t sw_amx(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, DispPartial part,
+                  hipStream_t s);
+
 hipError_t launch_disp_partials(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                                 DispPartial part, hipStream_t s);
 // window layout, D + 1 <= 257: the tile kernel writes ONE partial per pixel (all diagonals)

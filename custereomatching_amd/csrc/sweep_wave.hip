@@ -31,15 +31,20 @@
 #include "common.h"
 #include "sweep.h"
 
+// Build: compiled once per kernel size with -DCUSTMA_SW_K=<k> (the kernels and launchers of
+// that size: sw_fwd<k>, sw_amx<k>) and once with -DCUSTMA_SW_DISPATCH (grid planning and the
+// run-time dispatch over k), so the instantiations compile in parallel.
 namespace custma {
 
+constexpr int kTileMaxChunks = 4;  // k_fwd_tile: diagonal chunks (waves) per workgroup
+
+#ifndef CUSTMA_SW_DISPATCH
 namespace {
 
 typedef __attribute__((address_space(3))) volatile double lds_vd;
 typedef __attribute__((address_space(3))) volatile float lds_vf;
 
 constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
-constexpr int kTileMaxChunks = 4;  // k_fwd_tile: diagonal chunks (waves) per workgroup
 
 // REM: this wave (window layout, last chunk, (D+1) % 64 == 1) also computes the single
 // remainder diagonal d0 + 64 = D: lane x < 16 + 2r keeps its column sum, the horizontal box
@@ -508,30 +513,28 @@ hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats
     return hipGetLastError();
 }
 
-template <typename T>
-hipError_t dispatch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, DispPartial part,
-                        hipStream_t s) {
-    switch (g.k) {
-#define CUSTMA_K(KK) \
-    case KK: return launch_amx<KK, T>(cam, proj, g, sc, sp, part, s);
-        CUSTMA_SWEEP_KS(CUSTMA_K)
-#undef CUSTMA_K
-        default: return hipErrorInvalidValue;
-    }
-}
-
-template <typename T>
-hipError_t dispatch(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out, hipStream_t s) {
-    switch (g.k) {
-#define CUSTMA_K(KK) \
-    case KK: return launch_k<KK, T>(cam, proj, g, sc, sp, out, s);
-        CUSTMA_SWEEP_KS(CUSTMA_K)
-#undef CUSTMA_K
-        default: return hipErrorInvalidValue;
-    }
-}
-
 }  // namespace
+
+template <int K>
+hipError_t sw_fwd(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, float* out,
+                  hipStream_t s) {
+    if (dtype == CUSTMA_F16) return launch_k<K, __half>((const __half*)cam, (const __half*)proj, g, sc, sp, out, s);
+    return launch_k<K, float>((const float*)cam, (const float*)proj, g, sc, sp, out, s);
+}
+template <int K>
+hipError_t sw_amx(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, DispPartial part,
+                  hipStream_t s) {
+    if (dtype == CUSTMA_F16) return launch_amx<K, __half>((const __half*)cam, (const __half*)proj, g, sc, sp, part, s);
+    return launch_amx<K, float>((const float*)cam, (const float*)proj, g, sc, sp, part, s);
+}
+#ifdef CUSTMA_SW_K
+template hipError_t sw_fwd<CUSTMA_SW_K>(const void*, const void*, int, const Geo&, Stats, Stats, float*, hipStream_t);
+template hipError_t sw_amx<CUSTMA_SW_K>(const void*, const void*, int, const Geo&, Stats, Stats, DispPartial,
+                                        hipStream_t);
+#endif
+
+#else  // CUSTMA_SW_DISPATCH
+
 
 WaveGrid wave_grid(const Geo& g) {
     WaveGrid wg;
@@ -558,8 +561,13 @@ bool disp_tile_ok(const Geo& g) {
 
 hipError_t launch_disp_tile(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             DispPartial part, hipStream_t s) {
-    if (dtype == CUSTMA_F16) return dispatch_amx((const __half*)cam, (const __half*)proj, g, sc, sp, part, s);
-    return dispatch_amx((const float*)cam, (const float*)proj, g, sc, sp, part, s);
+    switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: return sw_amx<KK>(cam, proj, dtype, g, sc, sp, part, s);
+        CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
@@ -570,8 +578,14 @@ hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const G
     const char* e = getenv("CUSTMA_FWD_LDS");
     const bool lds = e ? atoi(e) != 0 : g.layout != CUSTMA_LAYOUT_WINDOW;
     if (lds) return launch_fwd_lds(cam, proj, dtype, g, sc, sp, out, s);
-    if (dtype == CUSTMA_F16) return dispatch((const __half*)cam, (const __half*)proj, g, sc, sp, out, s);
-    return dispatch((const float*)cam, (const float*)proj, g, sc, sp, out, s);
+    switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: return sw_fwd<KK>(cam, proj, dtype, g, sc, sp, out, s);
+        CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+        default: return hipErrorInvalidValue;
+    }
 }
+#endif  // CUSTMA_SW_DISPATCH
 
 }  // namespace custma
