@@ -173,6 +173,58 @@ __device__ __forceinline__ void asm_ld4(uint32_t& a0, uint32_t& a1, uint32_t& a2
         : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
         : "v"(oA), "v"(oB), "v"(oC), "v"(oD), "s"(r0), "s"(r1), "s"(r2));
 }
+// Image-row groups for the forward sweep: 8 image loads (projector enter/leave x 2 halves,
+// camera enter/leave x 2 halves) / 6 statistics loads, rows selected by SGPR soffsets.
+// `s_nop 4` first: the soffsets may have been written by a VALU op (hazard note above).
+template <typename T>
+__device__ __forceinline__ void asm_ld_img8(uint32_t& pe0, uint32_t& pe1, uint32_t& pl0, uint32_t& pl1,
+                                            uint32_t& ce0, uint32_t& ce1, uint32_t& cl0, uint32_t& cl1,
+                                            uint32_t vP0, uint32_t vP1, uint32_t vC0, uint32_t vC1, i32x4 dP,
+                                            i32x4 dC, uint32_t sE, uint32_t sL) {
+    if constexpr (sizeof(T) == 4) {
+        asm volatile(
+            "s_nop 4\n\t"
+            "buffer_load_dword %0, %8, %12, %14 offen\n\t"
+            "buffer_load_dword %1, %9, %12, %14 offen\n\t"
+            "buffer_load_dword %2, %8, %12, %15 offen\n\t"
+            "buffer_load_dword %3, %9, %12, %15 offen\n\t"
+            "buffer_load_dword %4, %10, %13, %14 offen\n\t"
+            "buffer_load_dword %5, %11, %13, %14 offen\n\t"
+            "buffer_load_dword %6, %10, %13, %15 offen\n\t"
+            "buffer_load_dword %7, %11, %13, %15 offen"
+            : "=&v"(pe0), "=&v"(pe1), "=&v"(pl0), "=&v"(pl1), "=&v"(ce0), "=&v"(ce1), "=&v"(cl0), "=&v"(cl1)
+            : "v"(vP0), "v"(vP1), "v"(vC0), "v"(vC1), "s"(dP), "s"(dC), "s"(sE), "s"(sL));
+    } else {
+        asm volatile(
+            "s_nop 4\n\t"
+            "buffer_load_ushort %0, %8, %12, %14 offen\n\t"
+            "buffer_load_ushort %1, %9, %12, %14 offen\n\t"
+            "buffer_load_ushort %2, %8, %12, %15 offen\n\t"
+            "buffer_load_ushort %3, %9, %12, %15 offen\n\t"
+            "buffer_load_ushort %4, %10, %13, %14 offen\n\t"
+            "buffer_load_ushort %5, %11, %13, %14 offen\n\t"
+            "buffer_load_ushort %6, %10, %13, %15 offen\n\t"
+            "buffer_load_ushort %7, %11, %13, %15 offen"
+            : "=&v"(pe0), "=&v"(pe1), "=&v"(pl0), "=&v"(pl1), "=&v"(ce0), "=&v"(ce1), "=&v"(cl0), "=&v"(cl1)
+            : "v"(vP0), "v"(vP1), "v"(vC0), "v"(vC1), "s"(dP), "s"(dC), "s"(sE), "s"(sL));
+    }
+}
+__device__ __forceinline__ void asm_ld_stat6(double& m0, double& m1, uint32_t& q0, uint32_t& q1, double& ub,
+                                             uint32_t& uq, uint32_t vM0, uint32_t vM1, uint32_t vQ0, uint32_t vQ1,
+                                             uint32_t vUB, uint32_t vUQ, i32x4 dPB, i32x4 dPS, i32x4 dCB, i32x4 dCS,
+                                             uint32_t s8, uint32_t s4) {
+    asm volatile(
+        "s_nop 4\n\t"
+        "buffer_load_dwordx2 %0, %6, %12, %16 offen\n\t"
+        "buffer_load_dwordx2 %1, %7, %12, %16 offen\n\t"
+        "buffer_load_dword %2, %8, %13, %17 offen\n\t"
+        "buffer_load_dword %3, %9, %13, %17 offen\n\t"
+        "buffer_load_dwordx2 %4, %10, %14, %16 offen\n\t"
+        "buffer_load_dword %5, %11, %15, %17 offen"
+        : "=&v"(m0), "=&v"(m1), "=&v"(q0), "=&v"(q1), "=&v"(ub), "=&v"(uq)
+        : "v"(vM0), "v"(vM1), "v"(vQ0), "v"(vQ1), "v"(vUB), "v"(vUQ), "s"(dPB), "s"(dPS), "s"(dCB), "s"(dCS),
+          "s"(s8), "s"(s4));
+}
 __device__ __forceinline__ void asm_ld_f64(double& d, uint32_t off, i32x4 r) {
     asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(d) : "v"(off), "s"(r));
 }

@@ -74,13 +74,21 @@ __device__ __forceinline__ void fmac2_bc64_x2(double& c0, double& c1, double a, 
         : "v"(a), "v"(b), "v"(pa0), "v"(pa1), "v"(pb0), "v"(pb1), "i"(L), "i"(L + 1));
 }
 // e += bcast(nb, lane L) * mv;  den2 += bcast(uq, lane L) * qv  (the finalisation's two DPP FMAs)
-template <int L>
+// NOP = false: the caller guarantees nb and uq were not written by the previous two VALU
+// instructions (e.g. every call after the first of a step, nb / uq being step constants).
+template <int L, bool NOP = true>
 __device__ __forceinline__ void fin_bc(double& e, float& den2, double nb, double mv, float uq, float qv) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %2, %3 row_newbcast:%6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %1, %4, %5 row_newbcast:%6 row_mask:0xf bank_mask:0xf"
-        : "+v"(e), "+v"(den2)
-        : "v"(nb), "v"(mv), "v"(uq), "v"(qv), "i"(L));
+    if constexpr (NOP)
+        asm("s_nop 1\n\t"
+            "v_fmac_f64_dpp %0, %2, %3 row_newbcast:%6 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %1, %4, %5 row_newbcast:%6 row_mask:0xf bank_mask:0xf"
+            : "+v"(e), "+v"(den2)
+            : "v"(nb), "v"(mv), "v"(uq), "v"(qv), "i"(L));
+    else
+        asm("v_fmac_f64_dpp %0, %2, %3 row_newbcast:%6 row_mask:0xf bank_mask:0xf\n\t"
+            "v_fmac_f32_dpp %1, %4, %5 row_newbcast:%6 row_mask:0xf bank_mask:0xf"
+            : "+v"(e), "+v"(den2)
+            : "v"(nb), "v"(mv), "v"(uq), "v"(qv), "i"(L));
 }
 
 // Kernel sizes with a compile-time sweep instantiation (register-resident

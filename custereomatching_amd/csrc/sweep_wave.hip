@@ -60,12 +60,15 @@ constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
 // AMX > 0 (STAGED, fused disparity): no volume; after the barrier each 16-lane group scans
 // one of the 16 LDS rows (all D+1 diagonals of one camera pixel) for (best, second, first
 // index of best), AMX passes of 4 rows per wave, and writes them as one disparity partial.
-template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2, int AMX = 0>
+// AMX < 0: fused disparity with the soft-argmax sums (DispPartial::s0 / s1), -AMX passes.
+template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2, int AMX_ = 0>
 __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
                                           const Stats& sc, const Stats& sp, float* __restrict__ out,
                                           int64_t u0, int64_t h0, int64_t h1, int64_t d0,
                                           double* rowE, double* rowL, double* sM, float* sQ, double* sR,
                                           float* stage = nullptr, DispPartial part = DispPartial{}) {
+    constexpr int AMX = AMX_ < 0 ? -AMX_ : AMX_;
+    constexpr bool SOFT = AMX_ < 0;
     constexpr int R = K / 2, NX = TW + 2 * R;
     static_assert(NX + 63 <= kRowP && NX <= 32, "row segment fits the LDS slice and two broadcast registers");
     constexpr uint32_t OOB = 0x80000000u;
@@ -87,9 +90,26 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     const uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 64, oS + 64 + l, 8);
     const uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 64, oS + 64 + l, 4);
     const uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
-    auto row_rsrc = [&](const void* base, int64_t row, int esz, bool ok) {
-        ok = ok && row >= 0 && row < g.H;
-        return make_rsrc_sgpr((const char*)base + (ok ? row : 0) * g.W * esz, ok ? (uint32_t)(g.W * esz) : 0u);
+    // Rows by SGPR soffset from one descriptor per array, based at the band's first row rb
+    // (so every offset stays small whatever the image size); a row outside the image gets
+    // soffset OOBS, past num_records (<= OOBS), so its loads read 0 -- also when the lane's
+    // column offset is OOB itself (0x80000000 + OOBS does not wrap).
+    constexpr uint32_t OOBS = 0x7FFFFFF0u;
+    const int Hi = (int)g.H, h0i = (int)h0, h1i = (int)h1;
+    const int rb = max(0, h0i - 3 * R - 1);
+    const uint32_t rbT = (uint32_t)(g.W * sizeof(T)), rb8 = (uint32_t)(g.W * 8), rb4 = (uint32_t)(g.W * 4);
+    auto band_rsrc = [&](const void* base, uint32_t rowbytes) {
+        const uint64_t n = (uint64_t)(g.H - rb) * rowbytes;
+        return make_rsrc_sgpr((const char*)base + (int64_t)rb * rowbytes, n < OOBS ? (uint32_t)n : OOBS);
+    };
+    const i32x4 dCam = band_rsrc(cam, rbT), dProj = band_rsrc(proj, rbT);
+    const i32x4 dPB = band_rsrc(sp.box, rb8), dPS = band_rsrc(sp.sq, rb4);
+    const i32x4 dCB = band_rsrc(sc.box, rb8), dCS = band_rsrc(sc.sq, rb4);
+    // (wave-uniform; readfirstlane pins it to an SGPR for the asm loads, whose `s_nop 4`
+    // covers the VALU-writes-SGPR hazard)
+    auto so_row = [&](int row, uint32_t rowbytes, bool ok) -> uint32_t {
+        return (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)((ok && (unsigned)row < (unsigned)Hi) ? (uint32_t)(row - rb) * rowbytes : OOBS));
     };
 
     struct Stage {
@@ -100,31 +120,13 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     // step t adds image row t+R and removes row t-R-1 (rows from h0-R on were added, so the
     // first removal is at t = h0+1); statistics of row t (only for t in [h0, h1))
     auto load_step = [&](int64_t t, Stage& p) {
-        const bool rem = t > h0;
-        const auto rCe = row_rsrc(cam, t + R, sizeof(T), true), rCl = row_rsrc(cam, t - R - 1, sizeof(T), rem);
-        const auto rPe = row_rsrc(proj, t + R, sizeof(T), true), rPl = row_rsrc(proj, t - R - 1, sizeof(T), rem);
-        asm_ld_raw<T>(p.pe0, vP0, rPe);
-        asm_ld_raw<T>(p.pe1, vP1, rPe);
-        asm_ld_raw<T>(p.pl0, vP0, rPl);
-        asm_ld_raw<T>(p.pl1, vP1, rPl);
-        asm_ld_raw<T>(p.ce0, vC0, rCe);
-        asm_ld_raw<T>(p.ce1, vC1, rCe);
-        asm_ld_raw<T>(p.cl0, vC0, rCl);
-        asm_ld_raw<T>(p.cl1, vC1, rCl);
-        const bool st = t >= h0 && t < h1;
-#ifdef CUSTMA_ABL_STATS7  // ablation builds only: statistics always from row 7 (L2-resident)
-        const int64_t ts = 7;
-#else
-        const int64_t ts = t;
-#endif
-        const auto rPB = row_rsrc(sp.box, ts, 8, st), rPS = row_rsrc(sp.sq, ts, 4, st);
-        const auto rCB = row_rsrc(sc.box, ts, 8, st), rCS = row_rsrc(sc.sq, ts, 4, st);
-        asm_ld_f64(p.m0, vM0, rPB);
-        asm_ld_f64(p.m1, vM1, rPB);
-        asm_ld_raw<float>(p.q0, vQ0, rPS);
-        asm_ld_raw<float>(p.q1, vQ1, rPS);
-        asm_ld_f64(p.ub, vUB, rCB);
-        asm_ld_raw<float>(p.uq, vUQ, rCS);
+        const int ti = (int)t;
+        const uint32_t sE = so_row(ti + R, rbT, true), sL = so_row(ti - R - 1, rbT, ti > h0i);
+        asm_ld_img8<T>(p.pe0, p.pe1, p.pl0, p.pl1, p.ce0, p.ce1, p.cl0, p.cl1, vP0, vP1, vC0, vC1, dProj, dCam, sE,
+                       sL);
+        const bool st = ti >= h0i && ti < h1i;
+        asm_ld_stat6(p.m0, p.m1, p.q0, p.q1, p.ub, p.uq, vM0, vM1, vQ0, vQ1, vUB, vUQ, dPB, dPS, dCB, dCS,
+                     so_row(ti, rb8, st), so_row(ti, rb4, st));
     };
     auto tie = [&](Stage& p) {
         asm_tie(p.pe0); asm_tie(p.pe1); asm_tie(p.pl0); asm_tie(p.pl1);
@@ -141,6 +143,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     else if (!FULL_EDGE) vOut = (uint32_t)(a0 * 4);  // interior chunk: every voxel valid
     const int64_t nrow = min((int64_t)TW, g.WO - u0);
     const uint32_t tile_bytes = (uint32_t)(nrow * DO * 4);
+    // volume block of output row t: orow = out + ((t - h_lo) WO + u0) DO, advanced one row per
+    // output step (no 64-bit multiply per step)
+    float* orow = out + ((h0 - g.h_lo) * g.WO + u0) * DO;
+    const int64_t ostep = g.WO * DO;
     const int sstep = (int)((DO + (window ? 0 : 1)) * 4);  // soffset per tile row
 
     double col[NX];
@@ -156,11 +162,20 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     // issues, so a peeled prologue with another register assignment would be joined to the
     // loop by register copies -- reads of registers whose loads are still in flight.
     Stage st[P];
+    // EARLY: a step's loads (for step t + P) issued right after its barrier, before its block
+    // stores, so the wait for loads(t) does not wait for the stores of step t - 2.  Measured
+    // no faster on MI355X (C3 volume 1.257 vs 1.226 ms, the fused disparity 22 % slower), so
+    // off unless built with CUSTMA_TILE_EARLY (benchmarking only).
+#if defined(CUSTMA_TILE_EARLY) && !defined(CUSTMA_ABL_NOSTORE)
+    constexpr bool EARLY = STAGED && P == 2 && AMX == 0;
+#else
+    constexpr bool EARLY = false;
+#endif
     auto compute = [&](Stage& p, int64_t t) {
         // loads(t) were issued at the end of step t-P; after them, for each step s in
         // t-P+1 .. t-1: its stores (from step h0 on) and loads(s+P)
-        constexpr int ST = AMX > 0 ? 5 * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);  // stores/step
-        static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
+        constexpr int ST = AMX > 0 ? (SOFT ? 5 : 3) * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);
+        static_assert((P - 1) * (kLoads + ST) + (EARLY ? ST : 0) <= 63, "vmcnt holds the pipeline");
 #ifdef CUSTMA_ABL_NOWAIT  // ablation builds only: no wait for the loads (garbage values)
         asm_vmcnt<63>();
 #else
@@ -168,6 +183,11 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             if (t - 2 >= h0) asm_vmcnt<2 * (kLoads + ST)>();
             else if (t - 1 >= h0) asm_vmcnt<2 * kLoads + ST>();
             else asm_vmcnt<2 * kLoads>();
+        } else if constexpr (EARLY) {
+            // issued after loads(t): stores(t-2), loads(t+1), stores(t-1)
+            if (t - 2 >= h0) asm_vmcnt<kLoads + 2 * ST>();
+            else if (t - 1 >= h0) asm_vmcnt<kLoads + ST>();
+            else asm_vmcnt<kLoads>();
         } else {
             if (t - 1 >= h0) asm_vmcnt<kLoads + ST>();
             else asm_vmcnt<kLoads>();
@@ -233,7 +253,8 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             colR = __builtin_fma(cRl, *(const lds_vd*)(rowL + 64 + l), colR);
         }
         if (t >= h0) {
-            const auto rOut = make_rsrc(out + ((t - g.h_lo) * g.WO + u0) * DO, tile_bytes);
+            const auto rOut = make_rsrc(orow, tile_bytes);
+            orow += ostep;
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
 #pragma unroll
             for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
@@ -241,6 +262,11 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             const lds_vf* qrow = (const lds_vf*)(sQ + l);
             lds_vf* sb = (lds_vf*)(stage + (t & 1) * TW * DO);  // STAGED: this step's buffer
             const bool dv = d0 + l <= g.D;
+            // every lane of the chunk valid (all but a partial last chunk): unmasked stage writes,
+            // no per-output exec branch
+            const bool allv = d0 + 63 <= g.D;
+            auto outputs = [&](auto masked_c) {
+            constexpr bool MASKED = decltype(masked_c)::value;
             Unroll<0, TW>::run([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
                 if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
@@ -264,12 +290,15 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 (void)sb;
 #else
                 if constexpr (STAGED) {
-                    if (dv) sb[m * DO + d0 + l] = c;
+                    if (!MASKED || dv) sb[m * DO + d0 + l] = c;
                 } else
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, so,
                                                       CUSTMA_STORE_AUX);
 #endif
             });
+            };
+            if (!STAGED || allv) outputs(std::false_type{});
+            else outputs(std::true_type{});
             if constexpr (REM) {
                 // diagonal D for tile row m = lane: box over the column sums of lanes m .. m + 2R
                 sR[l] = colR;
@@ -293,6 +322,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 // every wave's part of the 16 rows is in LDS: store the block (256 contiguous
                 // bytes per wave instruction, the whole workgroup's instruction contiguous)
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if constexpr (EARLY) load_step(t + P, p);  // p is dead past the outputs
                 const int NT = (int)blockDim.x, tid = (int)threadIdx.x;
                 const int total = (int)(nrow * DO);
                 if constexpr (AMX > 0) {
@@ -302,7 +332,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                     const auto rB = make_rsrc(part.best + prow, pb), rS = make_rsrc(part.second + prow, pb);
                     const auto rI = make_rsrc(part.index + prow, pb);
                     // soft-argmax sums (null arrays: out-of-range stores, so the store count holds)
-                    const bool soft = part.s0 != nullptr;
+                    constexpr bool soft = SOFT;
                     const auto rQ0 = make_rsrc(soft ? part.s0 + prow : part.best, soft ? pb : 0u);
                     const auto rQ1 = make_rsrc(soft ? part.s1 + prow : part.best, soft ? pb : 0u);
                     const float kb = part.kb;
@@ -340,9 +370,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, b), rB, vo, 0u, 0);
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, sec), rS, vo, 0u, 0);
                         __builtin_amdgcn_raw_buffer_store_b32((unsigned int)(bi == INT_MAX ? -1 : bi), rI, vo, 0u, 0);
-                        const uint32_t vq = soft ? vo : OOB;
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, q0), rQ0, vq, 0u, 0);
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, q1), rQ1, vq, 0u, 0);
+                        if constexpr (soft) {
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, q0), rQ0, vo, 0u, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, q1), rQ1, vo, 0u, 0);
+                        }
                     }
                 } else if constexpr (SS < 0) {  // block base 16-byte aligned (checked at launch)
                     const int n4 = total >> 2;
@@ -376,7 +407,8 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     auto step = [&](auto kc, int64_t t) {
         Stage& p = st[decltype(kc)::value];
         if (t >= hs) compute(p, t);
-        load_step(t + P, p);  // past the band's end: harmless (rows out of range read zeros)
+        // past the band's end: harmless (rows out of range read zeros)
+        if (!(EARLY && t >= h0)) load_step(t + P, p);
     };
     int64_t t_first = hs - P;  // opaque: the warm-up iterations must not be peeled
     asm volatile("" : "+s"(t_first));
@@ -478,12 +510,13 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
         // ((t - h_lo) WO + u0) DO = 0 mod 4 for all t (u0 = 0 mod 16)
         const char* e4 = getenv("CUSTMA_FWD_X4");  // benchmarking only: 0 = dword stores
         const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0) && !(e4 && atoi(e4) == 0);
+        const dim3 blk(64 * wg.nChunk);
         if (x4)
-            hipLaunchKernelGGL((k_fwd_tile<K, T, true>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
-                               proj, g, sc, sp, out, wg, DispPartial{});
+            hipLaunchKernelGGL((k_fwd_tile<K, T, true>), dim3((unsigned)blocks), blk, lds, s, cam, proj, g, sc, sp,
+                               out, wg, DispPartial{});
         else
-            hipLaunchKernelGGL((k_fwd_tile<K, T, false>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
-                               proj, g, sc, sp, out, wg, DispPartial{});
+            hipLaunchKernelGGL((k_fwd_tile<K, T, false>), dim3((unsigned)blocks), blk, lds, s, cam, proj, g, sc, sp,
+                               out, wg, DispPartial{});
     } else {
         const int64_t blocks = (int64_t)wg.nBand * wg.nTile * wg.nChunk;
         hipLaunchKernelGGL((k_fwd_wave<K, T>), dim3((unsigned)blocks), dim3(64), 0, s, cam, proj, g, sc, sp, out,
@@ -500,15 +533,15 @@ hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats
     const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
     const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
     prof_begin(PROF_FWD, s);
-    if (wg.nChunk == 4)
-        hipLaunchKernelGGL((k_fwd_tile<K, T, false, 1>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
-                           proj, g, sc, sp, nullptr, wg, part);
-    else if (wg.nChunk >= 2)
-        hipLaunchKernelGGL((k_fwd_tile<K, T, false, 2>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
-                           proj, g, sc, sp, nullptr, wg, part);
-    else
-        hipLaunchKernelGGL((k_fwd_tile<K, T, false, 4>), dim3((unsigned)blocks), dim3(64 * wg.nChunk), lds, s, cam,
-                           proj, g, sc, sp, nullptr, wg, part);
+    const int passes = wg.nChunk == 4 ? 1 : wg.nChunk >= 2 ? 2 : 4;  // 16 rows over the waves, 4 per pass
+    auto go = [&](auto amx) {
+        hipLaunchKernelGGL((k_fwd_tile<K, T, false, decltype(amx)::value>), dim3((unsigned)blocks),
+                           dim3(64 * wg.nChunk), lds, s, cam, proj, g, sc, sp, nullptr, wg, part);
+    };
+    const bool soft = part.s0 != nullptr;  // soft-argmax sums requested
+    if (passes == 1) soft ? go(std::integral_constant<int, -1>{}) : go(std::integral_constant<int, 1>{});
+    else if (passes == 2) soft ? go(std::integral_constant<int, -2>{}) : go(std::integral_constant<int, 2>{});
+    else soft ? go(std::integral_constant<int, -4>{}) : go(std::integral_constant<int, 4>{});
     prof_end(PROF_FWD, s);
     return hipGetLastError();
 }

@@ -16,6 +16,7 @@ VARIANTS = {
     "nostore": (["CUSTMA_ABL_NOSTORE"], FWD), "noupdate": (["CUSTMA_ABL_NOUPDATE"], FWD),
     "storeonly": (["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT"], FWD),
     "nowait": (["CUSTMA_ABL_NOWAIT"], FWD), "stats7": (["CUSTMA_ABL_STATS7"], FWD),
+    "early": (["CUSTMA_TILE_EARLY"], FWD),
     # backward unit height / block order (bwd_fused.hip)
     "r16o1": (["CUSTMA_BWD_ROWS=16", "CUSTMA_BWD_ORDER=1"], BWD),
     "r16o2": (["CUSTMA_BWD_ROWS=16", "CUSTMA_BWD_ORDER=2"], BWD),
