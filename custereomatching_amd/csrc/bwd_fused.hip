@@ -134,6 +134,7 @@ struct BwdArgs {
     float* part;         // [NTYPE][S][H][W]
     const int* cover;    // k_bwd_cover: slot counts and lists per (range class, column)
     int S, Sj, nChunk, nRG, jc, nsegMax;
+    int order;  // block order of k_bwd_coop (see there)
     int64_t dlo, ylo, yhi;
 };
 
@@ -166,9 +167,6 @@ constexpr int NWC = TRB / TRW;   // waves per cooperative workgroup
 #define CUSTMA_BWD_DEPTH 1  // 2 measured no faster (C2 full 5.37 vs 5.19 ms): latency is not the limit
 #endif
 constexpr int BDP = CUSTMA_BWD_DEPTH;  // steps of loads in flight (1 or 2)
-#ifndef CUSTMA_BWD_ORDER
-#define CUSTMA_BWD_ORDER 2
-#endif
 #ifndef CUSTMA_BWD_SLIDE
 #define CUSTMA_BWD_SLIDE 1
 #endif
@@ -550,31 +548,29 @@ __global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
     // A wave's 256-byte gradient / volume row segment spans three 128-byte lines whose outer
     // parts the neighbouring diagonal chunk's workgroup reads at the same step; the order
     // decides whether those reads meet in the XCD's L2.
-    // CUSTMA_BWD_ORDER 2 (default): on an XCD, chunk rank fastest, then row group, then
-    //   segment -- the chunks of one (row group, segment) are dispatched together.
-    // 1: row group fastest, then chunk rank, then segment.  0: row group, segment, chunk.
+    // a.order 2 (window layouts): on an XCD, chunk rank fastest, then row group, then segment
+    //   -- the few chunks of one (row group, segment) are dispatched together (C5 window:
+    //   FETCH 140 -> 103 GB per launch, 37.1 -> 35.7 ms op).
+    // a.order 1 (full layout, up to 2W/64 chunks of very different lengths): row group fastest,
+    //   then chunk rank (longest first), then segment (C2 full: 4.36 -> 3.85-4.05 ms op).
     const int64_t hb = blockIdx.x, xi = hb / 8, x = hb % 8;
     const int nRGx = (a.nRG + 7) / 8;
-#if CUSTMA_BWD_ORDER == 2
-    const int jr = (int)(xi % a.nChunk);
-    const int64_t rest = xi / a.nChunk;
-    const int rg = (int)(x * nRGx + rest % nRGx);
-    const int64_t sg64 = rest / nRGx;
-    if (rg >= a.nRG || sg64 >= a.nsegMax) return;
-    const int j = chunk_of_rank(jr, a.nChunk, a.jc);
-    const int sg = (int)sg64;
-#else
-    const int64_t unit = xi / nRGx;
-    const int rg = (int)(x * nRGx + xi % nRGx);
-    if (rg >= a.nRG || unit >= (int64_t)a.nChunk * a.nsegMax) return;
-#if CUSTMA_BWD_ORDER == 1
-    const int j = chunk_of_rank((int)(unit % a.nChunk), a.nChunk, a.jc);
-    const int sg = (int)(unit / a.nChunk);
-#else
-    const int j = chunk_of_rank((int)(unit / a.nsegMax), a.nChunk, a.jc);
-    const int sg = (int)(unit % a.nsegMax);
-#endif
-#endif
+    int j, sg, rg;
+    if (a.order == 2) {
+        const int jr = (int)(xi % a.nChunk);
+        const int64_t rest = xi / a.nChunk;
+        rg = (int)(x * nRGx + rest % nRGx);
+        const int64_t sg64 = rest / nRGx;
+        if (rg >= a.nRG || sg64 >= a.nsegMax) return;
+        j = chunk_of_rank(jr, a.nChunk, a.jc);
+        sg = (int)sg64;
+    } else {
+        const int64_t unit = xi / nRGx;
+        rg = (int)(x * nRGx + xi % nRGx);
+        if (rg >= a.nRG || unit >= (int64_t)a.nChunk * a.nsegMax) return;
+        j = chunk_of_rank((int)(unit % a.nChunk), a.nChunk, a.jc);
+        sg = (int)(unit / a.nChunk);
+    }
     if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
     constexpr int NY = TRB + 2 * (K / 2);
     __shared__ __attribute__((aligned(16))) float Abuf[2 * NY * 64];
@@ -946,6 +942,8 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     a.Xc = prep; a.mcc = prep + n; a.cc = prep + 2 * n; a.Yp = prep + 3 * n; a.mpp = prep + 4 * n; a.pp = prep + 5 * n;
     a.S = p.S; a.Sj = p.Sj; a.nChunk = p.nChunk; a.nRG = p.nRG; a.jc = p.jc; a.nsegMax = p.nsegMax;
     a.dlo = p.dlo; a.ylo = p.ylo; a.yhi = p.yhi;
+    a.order = g.layout == CUSTMA_LAYOUT_WINDOW ? 2 : 1;
+    if (const char* eo = getenv("CUSTMA_BWD_ORDER")) a.order = atoi(eo);  // benchmarking only
     const int64_t units = (int64_t)p.nChunk * p.nsegMax * p.nRG;
     const unsigned blocks = (unsigned)(8 * (int64_t)p.nChunk * p.nsegMax * cdiv(p.nRG, 8));
     if (units > 0) {

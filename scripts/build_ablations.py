@@ -18,10 +18,7 @@ VARIANTS = {
     "nowait": (["CUSTMA_ABL_NOWAIT"], FWD), "stats7": (["CUSTMA_ABL_STATS7"], FWD),
     "early": (["CUSTMA_TILE_EARLY"], FWD),
     # backward unit height / block order (bwd_fused.hip)
-    "r16o1": (["CUSTMA_BWD_ROWS=16", "CUSTMA_BWD_ORDER=1"], BWD),
-    "r16o2": (["CUSTMA_BWD_ROWS=16", "CUSTMA_BWD_ORDER=2"], BWD),
-    "r32o1": (["CUSTMA_BWD_ROWS=32", "CUSTMA_BWD_ORDER=1"], BWD),
-    "r32o2": (["CUSTMA_BWD_ROWS=32", "CUSTMA_BWD_ORDER=2"], BWD),
+    "r32": (["CUSTMA_BWD_ROWS=32"], BWD),  # block order: CUSTMA_BWD_ORDER=1|2 at run time
 }
 for n in (sys.argv[1:] or VARIANTS):
     d, only = VARIANTS[n]
