@@ -224,8 +224,6 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     const float cb = a.shift[0], pb = a.shift[1];
 
     const uint32_t ib = (uint32_t)(plane * 4);
-    const auto rXc = make_rsrc(a.Xc, ib), rMc = make_rsrc(a.mcc, ib), rCc = make_rsrc(a.cc, ib);
-    const auto rYp = make_rsrc(a.Yp, ib), rMp = make_rsrc(a.mpp, ib), rPp = make_rsrc(a.pp, ib);
     const size_t slab = (size_t)g.WO * g.DO;
     const int64_t vrow0 = max(g.h_lo, y0 - R);
     const auto rG = make_rsrc(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
@@ -233,6 +231,17 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     const int64_t ir0 = y0 - R;
     const uint32_t vstride = (uint32_t)(slab * 4);
     const int hlo = (int)g.h_lo, hhi = (int)g.h_hi, vrow0i = (int)vrow0;
+    // The six prepared images are one array (k_bwd_prep: X, mc', c, Y, mp', p) read through ONE
+    // descriptor, the image selected by a per-lane offset: two descriptors instead of eight keep
+    // the kernel's SGPRs (spilled to VGPR lanes before) in registers.
+    enum { kX = 0, kMc = 1, kC = 2, kY = 3, kMp = 4, kP = 5 };
+    const uint32_t pb4 = ib;  // bytes per prepared image
+    auto img_off_a = [&](int row, int col, int arr) -> uint32_t {
+        return (row >= 0 && row < Hi && col >= 0 && col < Wi) ? (uint32_t)((row * Wi + col) * 4) + arr * pb4 : kOOB;
+    };
+    auto col_off_a = [&](int col, int arr) -> uint32_t {
+        return (col >= 0 && col < Wi) ? (uint32_t)(col * 4) + arr * pb4 : kOOB;
+    };
     auto img_off = [&](int row, int col) -> uint32_t {
         return (row >= 0 && row < Hi && col >= 0 && col < Wi) ? (uint32_t)((row * Wi + col) * 4) : kOOB;
     };
@@ -318,8 +327,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     }
     const i32x4 dG = make_rsrc_sgpr(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
     const i32x4 dV = make_rsrc_sgpr(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
-    const i32x4 dY = make_rsrc_sgpr(a.Yp, ib), dM = make_rsrc_sgpr(a.mpp, ib), dP = make_rsrc_sgpr(a.pp, ib);
-    const i32x4 dX = make_rsrc_sgpr(a.Xc, ib), dMc = make_rsrc_sgpr(a.mcc, ib), dCc = make_rsrc_sgpr(a.cc, ib);
+    const i32x4 dPr = make_rsrc_sgpr(a.Xc, 6u * ib);  // a.Xc = the prepared array's base
     struct Ld {
         uint32_t ge[TRW], cv[TRW], Ye[TRW], mp[TRW], pq[TRW], hg[HP], hY[HP], xr[NXR], mc, cx;
     };
@@ -327,7 +335,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         const int xb = w - R;
         const bool ve = w >= lwlo && w < lwhi;
         const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
-        const uint32_t oYe = col_off(w + dl), oPq = col_off(xb + dl);
+        const uint32_t oYe = col_off_a(w + dl, kY), oMe = col_off_a(w + dl, kMp), oPq = col_off_a(xb + dl, kP);
         if constexpr (SLIDE) {
 #pragma unroll
             for (int m = 0; m < TRW; ++m) asm_ld2s(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
@@ -335,33 +343,36 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             for (int i = 0; i < HP; ++i) asm_ld1s(b.hg[i], wv + NWC * i < NH ? oGe : kOOB, dG, sVh[i]);
         } else {
 #pragma unroll
-            for (int m = 0; m < TRW; ++m)
-                asm_ld5s(b.ge[m], b.cv[m], b.Ye[m], b.mp[m], b.pq[m], oGe, oYe, oPq, dG, dV, dY, dM, dP, sVo[m],
-                         sIo[m]);
+            for (int m = 0; m < TRW; ++m) {
+                asm_ld2s(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
+                asm_ld2s(b.Ye[m], b.mp[m], oYe, oMe, dPr, dPr, sIo[m], sIo[m]);
+                asm_ld1s(b.pq[m], oPq, dPr, sIo[m]);
+            }
 #pragma unroll
             for (int i = 0; i < HP; ++i) {
                 const bool ok = wv + NWC * i < NH;
-                asm_ld2s(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dY, sVh[i], sIh[i]);
+                asm_ld2s(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dPr, sVh[i], sIh[i]);
             }
         }
         const int r16 = lane & 15;
-        asm_ld4(b.xr[0], b.xr[1], b.mc, b.cx, r16 < NY ? img_off((int)ir0 + r16, w) : kOOB,
-                16 + r16 < NY ? img_off((int)ir0 + 16 + r16, w) : kOOB, img_off(y0i + yw + (lane & 3), w),
-                img_off(y0i + yw + (lane & 3), xb), dX, dMc, dCc);
-        if constexpr (NXR > 2) asm_ld1s(b.xr[2], 32 + r16 < NY ? img_off((int)ir0 + 32 + r16, w) : kOOB, dX, 0u);
+        asm_ld4(b.xr[0], b.xr[1], b.mc, b.cx, r16 < NY ? img_off_a((int)ir0 + r16, w, kX) : kOOB,
+                16 + r16 < NY ? img_off_a((int)ir0 + 16 + r16, w, kX) : kOOB,
+                img_off_a(y0i + yw + (lane & 3), w, kMc), img_off_a(y0i + yw + (lane & 3), xb, kC), dPr, dPr, dPr);
+        if constexpr (NXR > 2)
+            asm_ld1s(b.xr[2], 32 + r16 < NY ? img_off_a((int)ir0 + 32 + r16, w, kX) : kOOB, dPr, 0u);
     };
     // SLIDE: the current step's projector-side columns (lane l: column w + dl, p': w - R + dl)
     // and the once-per-64-steps column block whose lane i feeds lane 63 at step w0 + 1 + 64k + i
     uint32_t sY[TRW], sMp[TRW], sPq[TRW], shY[HP], bY[TRW], bMp[TRW], bPq[TRW], bhY[HP];
     auto load_cols = [&](uint32_t* Y, uint32_t* Mp, uint32_t* Pq, uint32_t* hY, int cb) {
-        const uint32_t oY = col_off(cb + dl), oP = col_off(cb - R + dl);
+        const uint32_t oY = col_off_a(cb + dl, kY), oM = col_off_a(cb + dl, kMp), oP = col_off_a(cb - R + dl, kP);
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
-            asm_ld2s(Y[m], Mp[m], oY, oY, dY, dM, sIo[m], sIo[m]);
-            asm_ld1s(Pq[m], oP, dP, sIo[m]);
+            asm_ld2s(Y[m], Mp[m], oY, oM, dPr, dPr, sIo[m], sIo[m]);
+            asm_ld1s(Pq[m], oP, dPr, sIo[m]);
         }
 #pragma unroll
-        for (int i = 0; i < HP; ++i) asm_ld1s(hY[i], wv + NWC * i < NH ? oY : kOOB, dY, sIh[i]);
+        for (int i = 0; i < HP; ++i) asm_ld1s(hY[i], wv + NWC * i < NH ? oY : kOOB, dPr, sIh[i]);
     };
     auto tie_cols = [&]() {
 #pragma unroll
@@ -985,6 +996,8 @@ size_t backward_workspace_bytes(const Geo& g) {
 }
 
 bool backward_supported(const Geo& g) {
+    // the six prepared fp32 images are addressed through one 32-bit buffer range
+    if ((double)g.H * (double)g.W * 24.0 >= 2147483648.0) return false;
     // 32-bit buffer offsets: the volume rows one wave reads (16 + 2r + 1 row slabs) and one fp64
     // image must stay below 2 GiB
     if (!plan_bwd(g).ok) return false;
