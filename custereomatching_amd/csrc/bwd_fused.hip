@@ -195,8 +195,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
                                               float* ring, float (*cbuf)[12], float (*pbuf)[12]) {
     constexpr int R = K / 2, NY = TRB + 2 * R, NH = 2 * R;  // NH halo rows
     constexpr int HPW = (NH + NWC - 1) / NWC;                // halo rows per wave (at most)
-    constexpr int NXR = (NY + 15) / 16;  // row-replicated registers holding X of the NY rows
-    static_assert(NXR <= 3, "three row-replicated registers cover the rows");
+    static_assert(HPW <= 4, "a wave's halo rows fit one quad of a 16-lane row");
 
     const ChunkGeo cg = chunk_geo(g, a.dlo, j);
     const int lane = threadIdx.x & 63;
@@ -328,8 +327,13 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     const i32x4 dG = make_rsrc_sgpr(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
     const i32x4 dV = make_rsrc_sgpr(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
     const i32x4 dPr = make_rsrc_sgpr(a.Xc, 6u * ib);  // a.Xc = the prepared array's base
+    const int orow_l = y0i + yw + (lane & 3);  // own image row of this lane's quad slot
+    int hrow_l = -1;                           // halo image row of this lane's quad slot (or none)
+    if ((lane & 3) < HPW && wv + NWC * (lane & 3) < NH) hrow_l = (int)ir0 + halo_row(wv + NWC * (lane & 3));
     struct Ld {
-        uint32_t ge[TRW], cv[TRW], Ye[TRW], mp[TRW], pq[TRW], hg[HP], hY[HP], xr[NXR], mc, cx;
+        // xo / mc / cx: lane l holds own row l & 3 (row-replicated per 16 lanes, read back with
+        // DPP row_newbcast); xh: lane l holds the wave's halo row l & 3
+        uint32_t ge[TRW], cv[TRW], Ye[TRW], mp[TRW], pq[TRW], hg[HP], hY[HP], xo, xh, mc, cx;
     };
     auto issue = [&](int w, Ld& b) {
         const int xb = w - R;
@@ -354,12 +358,8 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
                 asm_ld2s(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dPr, sVh[i], sIh[i]);
             }
         }
-        const int r16 = lane & 15;
-        asm_ld4(b.xr[0], b.xr[1], b.mc, b.cx, r16 < NY ? img_off_a((int)ir0 + r16, w, kX) : kOOB,
-                16 + r16 < NY ? img_off_a((int)ir0 + 16 + r16, w, kX) : kOOB,
-                img_off_a(y0i + yw + (lane & 3), w, kMc), img_off_a(y0i + yw + (lane & 3), xb, kC), dPr, dPr, dPr);
-        if constexpr (NXR > 2)
-            asm_ld1s(b.xr[2], 32 + r16 < NY ? img_off_a((int)ir0 + 32 + r16, w, kX) : kOOB, dPr, 0u);
+        asm_ld4(b.xo, b.xh, b.mc, b.cx, img_off_a(orow_l, w, kX), hrow_l >= 0 ? img_off_a(hrow_l, w, kX) : kOOB,
+                img_off_a(orow_l, w, kMc), img_off_a(orow_l, xb, kC), dPr, dPr, dPr);
     };
     // SLIDE: the current step's projector-side columns (lane l: column w + dl, p': w - R + dl)
     // and the once-per-64-steps column block whose lane i feeds lane 63 at step w0 + 1 + 64k + i
@@ -382,12 +382,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 #pragma unroll
         for (int i = 0; i < HP; ++i) { asm_tie(shY[i]); asm_tie(bhY[i]); }
     };
-    auto slide1 = [&](uint32_t v, uint32_t b, int idx) -> uint32_t {
-        int sh = __builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);  // lane l <- v[l+1]
-        const int nv = __builtin_amdgcn_readlane((int)b, idx);
-        asm volatile("v_writelane_b32 %0, %1, 63" : "+v"(sh) : "s"(nv));
-        return (uint32_t)sh;
-    };
+    const uint64_t lane63 = 1ull << 63;
     auto tie = [&](Ld& b) {
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
@@ -399,16 +394,14 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             asm_tie(b.hg[i]);
             if constexpr (!SLIDE) asm_tie(b.hY[i]);
         }
-#pragma unroll
-        for (int i = 0; i < NXR; ++i) asm_tie(b.xr[i]);
-        asm_tie(b.mc); asm_tie(b.cx);
+        asm_tie(b.xo); asm_tie(b.xh); asm_tie(b.mc); asm_tie(b.cx);
         if constexpr (SLIDE) tie_cols();
     };
     auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
 
     int sidx = 0;  // ring slot of the current step (step count mod K)
     // loads per issue() (asm_ld5s / asm_ld2s / asm_ld4) and stores per flush(), per thread
-    constexpr int NL = (SLIDE ? TRW * 2 + HP : TRW * 5 + HP * 2) + 4 + (NXR > 2 ? 1 : 0), SF = 6;
+    constexpr int NL = (SLIDE ? TRW * 2 + HP : TRW * 5 + HP * 2) + 4, SF = 6;
     static_assert(NL + SF <= 63, "vmcnt holds the pipeline");
     // cur was issued BDP steps ago; issued since: the later steps' loads, and a flush's SF
     // stores after step s = FBC-1 of the previous block (flush() itself waits until only
@@ -423,15 +416,10 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         tie(cur);
         if constexpr (SLIDE) {
             if (w > w0) {  // move the columns down one lane; lane 63 takes column w + 63 (+ offset)
-                const int idx = (w - w0 - 1) & 63;
 #pragma unroll
-                for (int m = 0; m < TRW; ++m) {
-                    sY[m] = slide1(sY[m], bY[m], idx);
-                    sMp[m] = slide1(sMp[m], bMp[m], idx);
-                    sPq[m] = slide1(sPq[m], bPq[m], idx);
-                }
+                for (int m = 0; m < TRW; ++m) slide3(sY[m], sMp[m], sPq[m], bY[m], bMp[m], bPq[m], lane63);
 #pragma unroll
-                for (int i = 0; i < HP; ++i) shY[i] = slide1(shY[i], bhY[i], idx);
+                for (int i = 0; i < HP; ++i) slide1(shY[i], bhY[i], lane63);
             }
             // the block for steps w + 1 .. w + 64 (lane i -> step w + 1 + i): columns w + 64 + i (+ offset);
             // issued after this step's reads of the previous block
@@ -448,44 +436,31 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         const float tf = xb >= xs ? 1.f : 0.f, af = (w >= xs && w < xe) ? 1.f : 0.f;
         const float mco = F(cur.mc) * af;
         const float cxo = (F(cur.cx) - cb) * tf;
-        // X of unit row y (wave-uniform y): the lane of the row-replicated register that holds it
-        // (y is wave-uniform but not a compile-time constant: select, never index the register
-        // array dynamically -- that would spill it to scratch at the asm load's issue point)
-        auto xrow = [&](int y) -> float {
-            float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)cur.xr[0], y & 15));
-#pragma unroll
-            for (int i = 1; i < NXR; ++i) {
-                const float u = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)cur.xr[i], y & 15));
-                v = (y >> 4) == i ? u : v;
-            }
-            return v;
-        };
-        // ---- own rows: A, and the per-voxel terms (unit rows R + yw .. R + yw + 3) ----
+        // ---- own rows: A, and the per-voxel terms (unit rows R + yw .. R + yw + 3); the
+        // row's camera values come from quad slot m of the row-replicated registers ----
         float amv[TRW], bv[TRW];
-#pragma unroll
-        for (int m = 0; m < TRW; ++m) {
+        Unroll<0, TRW>::run([&](auto mi) {
+            constexpr int m = decltype(mi)::value;
             const int y = R + yw + m;
-            const float Xf = xrow(y), Ye = F(SLIDE ? sY[m] : cur.Ye[m]);
+            const float Xf = rbc<m>(F(cur.xo)), Ye = F(SLIDE ? sY[m] : cur.Ye[m]);
             const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, Ye, kEps));
             const float Ae = F(cur.ge[m]) * rSe;
             Acur[y * 64 + lane] = Ae;
             const float V = Ae * F(cur.cv[m]) * rSe;
             amv[m] = Ae * F(SLIDE ? sMp[m] : cur.mp[m]);
             bv[m] = V * Ye;
-            const float mcm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mco), m));
-            P[1][m] = shl1_add(P[1][m], Ae * mcm);
+            P[1][m] = shl1_add(P[1][m], Ae * rbc<m>(mco));
             P[2][m] = shl1_add(P[2][m], (V * af) * Xf);
-        }
-#pragma unroll
-        for (int i = 0; i < HPW; ++i) {
+        });
+        Unroll<0, HPW>::run([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
             const int q = wv + NWC * i;
             if (q < NH) {
                 const int y = halo_row(q);
-                const float Xf = xrow(y);
-                Acur[y * 64 + lane] =
-                    F(cur.hg[i]) * __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, F(SLIDE ? shY[i] : cur.hY[i]), kEps));
+                Acur[y * 64 + lane] = F(cur.hg[i]) * __builtin_amdgcn_rsqf(
+                                                         __builtin_fmaf(rbc<i>(F(cur.xh)), F(SLIDE ? shY[i] : cur.hY[i]), kEps));
             }
-        }
+        });
         __syncthreads();  // the unit's A rows of this step are published
         // ---- vertical k-row sums of own rows, horizontal slide through the ring ----
         float col[TRW + 2 * R];
@@ -495,16 +470,15 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 #pragma unroll
         for (int y = 0; y <= 2 * R; ++y) v += col[y];
         float t1v[TRW];
-#pragma unroll
-        for (int m = 0; m < TRW; ++m) {
+        Unroll<0, TRW>::run([&](auto mi) {
+            constexpr int m = decltype(mi)::value;
             if (m > 0) v = (v + col[m + 2 * R]) - col[m - 1];
             float* rs = ring + (sidx * TRW + m) * 64 + lane;  // V of row m, K steps ago
             HV[m] += v - *rs;
             *rs = v;
             t1v[m] = (F(SLIDE ? sPq[m] : cur.pq[m]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
-            const float cxm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxo), m));
-            P[0][m] = shl1_add(P[0][m], cxm * HV[m]);
-        }
+            P[0][m] = shl1_add(P[0][m], rbc<m>(cxo) * HV[m]);
+        });
         sidx = sidx + 1 == K ? 0 : sidx + 1;
         const float w0r = red16(red32(amv[0], bv[0]), red32(amv[1], bv[1]));
         const float w1r = red16(red32(amv[2], bv[2]), red32(amv[3], bv[3]));

@@ -10,6 +10,45 @@ __device__ __forceinline__ float bcast(float a) {  // lane L of each 16-lane row
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0x150 + L, 0xf, 0xf,
                                                                  false));
 }
+// The same broadcast with bound_ctrl set (row_newbcast has no out-of-range source lane, so
+// the value is identical): the form the compiler folds into the consuming VOP2 op
+// (v_mul_f32_dpp / v_add_f32_dpp), with its own hazard tracking.
+template <int L>
+__device__ __forceinline__ float rbc(float a) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0x150 + L, 0xf, 0xf,
+                                                                 true));
+}
+// Sliding column registers (backward sweep): v moves down one lane (lane l <- v[l + 1],
+// wave_shl:1) and its lane 63 takes lane 63 of the block register b, which first rotates
+// down one lane (wave_rol:1: lane l <- b[(l + 1) & 63]).  After its i-th rotation since it
+// was loaded, b's lane 63 holds the block's element i - 1, so a block loaded once feeds 64
+// steps at two VALU ops per register and step.  `s_nop 1`: a DPP source written by the
+// previous VALU op needs 2 wait states; VCC (the lane-63 select) is written by SALU.
+__device__ __forceinline__ void slide3(uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& b0, uint32_t& b1,
+                                       uint32_t& b2, uint64_t lane63) {
+    asm volatile(
+        "s_mov_b64 vcc, %6\n\t"
+        "s_nop 1\n\t"
+        "v_mov_b32_dpp %3, %3 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %4, %4 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %5, %5 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %0, %0, %3, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %1, %1, %4, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %2, %2, %5, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+        : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(b0), "+v"(b1), "+v"(b2)
+        : "s"(lane63)
+        : "vcc");
+}
+__device__ __forceinline__ void slide1(uint32_t& v, uint32_t& b, uint64_t lane63) {
+    asm volatile(
+        "s_mov_b64 vcc, %2\n\t"
+        "s_nop 1\n\t"
+        "v_mov_b32_dpp %1, %1 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %0, %0, %1, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+        : "+v"(v), "+v"(b)
+        : "s"(lane63)
+        : "vcc");
+}
 __device__ __forceinline__ float shl1_add(float acc, float v) {  // lane l <- acc[l+1] + v[l]; lane 63 <- v
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, acc), 0x130, 0xf, 0xf,
                                                                  true)) + v;
