@@ -22,6 +22,8 @@ SWEEP_KS = (1, 3, 5, 7, 9, 11, 13, 15)  # CUSTMA_SWEEP_KS in csrc/sweep.h
 UNITS = [(os.path.splitext(src)[0], src, []) for src in SOURCES if src != "sweep_wave.hip"]
 UNITS += [("sweep_wave_d", "sweep_wave.hip", ["-DCUSTMA_SW_DISPATCH"])]
 UNITS += [(f"sweep_wave_k{k}", "sweep_wave.hip", [f"-DCUSTMA_SW_K={k}"]) for k in SWEEP_KS]
+# translation units whose inline asm omits wait states where the listing shows none are needed
+HAZARD_CHECKED = ("bwd_fused.hip",)
 ARCH = os.environ.get("CUSTMA_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: fused multiply-adds only where written (__builtin_fmaf / fma);
@@ -46,7 +48,25 @@ def _compile(unit, extra=(), libdir=LIBDIR):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {name} ({src}):\n{r.stderr}")
+    if src in HAZARD_CHECKED:
+        _check_hazards(unit, extra, libdir)
     return out
+
+
+def _check_hazards(unit, extra, libdir):
+    """Inline asm that leaves out wait states (hazard_check.py) is only safe in the code the
+    compiler actually emitted: check the device listing of the same compile."""
+    name, src, defs = unit
+    listing = os.path.join(libdir, name + ".s")
+    cmd = [HIPCC, *CFLAGS, *defs, *extra, "--cuda-device-only", "-S", os.path.join(CSRC, src), "-o", listing]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc -S failed for {name} ({src}):\n{r.stderr}")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "hazard_check.py"), listing], capture_output=True, text=True)
+    if r.returncode != 0:
+        os.remove(_obj(unit, libdir))
+        raise RuntimeError(f"wait-state hazards in {name} ({src}):\n{r.stdout}")
+    os.remove(listing)
 
 
 def _headers():

@@ -335,41 +335,46 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         // DPP row_newbcast); xh: lane l holds the wave's halo row l & 3
         uint32_t ge[TRW], cv[TRW], Ye[TRW], mp[TRW], pq[TRW], hg[HP], hY[HP], xo, xh, mc, cx;
     };
-    auto issue = [&](int w, Ld& b) {
+    // NOP: open each load group with `s_nop 4` (VALU SGPR write -> VMEM read); the in-loop
+    // issues go without -- their descriptors / soffsets are loop constants, written (by
+    // readfirstlane) only in the prologue, which custereomatching_amd/hazard_check.py checks at build time
+    auto issue = [&](int w, Ld& b, auto nop_) {
+        constexpr bool NOP = decltype(nop_)::value;
         const int xb = w - R;
         const bool ve = w >= lwlo && w < lwhi;
         const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
         const uint32_t oYe = col_off_a(w + dl, kY), oMe = col_off_a(w + dl, kMp), oPq = col_off_a(xb + dl, kP);
         if constexpr (SLIDE) {
 #pragma unroll
-            for (int m = 0; m < TRW; ++m) asm_ld2s(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
+            for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
 #pragma unroll
-            for (int i = 0; i < HP; ++i) asm_ld1s(b.hg[i], wv + NWC * i < NH ? oGe : kOOB, dG, sVh[i]);
+            for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], wv + NWC * i < NH ? oGe : kOOB, dG, sVh[i]);
         } else {
 #pragma unroll
             for (int m = 0; m < TRW; ++m) {
-                asm_ld2s(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
-                asm_ld2s(b.Ye[m], b.mp[m], oYe, oMe, dPr, dPr, sIo[m], sIo[m]);
-                asm_ld1s(b.pq[m], oPq, dPr, sIo[m]);
+                asm_ld2s<NOP>(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
+                asm_ld2s<NOP>(b.Ye[m], b.mp[m], oYe, oMe, dPr, dPr, sIo[m], sIo[m]);
+                asm_ld1s<NOP>(b.pq[m], oPq, dPr, sIo[m]);
             }
 #pragma unroll
             for (int i = 0; i < HP; ++i) {
                 const bool ok = wv + NWC * i < NH;
-                asm_ld2s(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dPr, sVh[i], sIh[i]);
+                asm_ld2s<NOP>(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dPr, sVh[i], sIh[i]);
             }
         }
-        asm_ld4(b.xo, b.xh, b.mc, b.cx, img_off_a(orow_l, w, kX), hrow_l >= 0 ? img_off_a(hrow_l, w, kX) : kOOB,
+        asm_ld4<NOP>(b.xo, b.xh, b.mc, b.cx, img_off_a(orow_l, w, kX), hrow_l >= 0 ? img_off_a(hrow_l, w, kX) : kOOB,
                 img_off_a(orow_l, w, kMc), img_off_a(orow_l, xb, kC), dPr, dPr, dPr);
     };
     // SLIDE: the current step's projector-side columns (lane l: column w + dl, p': w - R + dl)
     // and the once-per-64-steps column block whose lane i feeds lane 63 at step w0 + 1 + 64k + i
-    uint32_t sY[TRW], sMp[TRW], sPq[TRW], shY[HP], bY[TRW], bMp[TRW], bPq[TRW], bhY[HP];
-    auto load_cols = [&](uint32_t* Y, uint32_t* Mp, uint32_t* Pq, uint32_t* hY, int cb) {
+    // sc[3m + {0, 1, 2}] = Y, mp', p' of own row m; bc the same for the block
+    uint32_t sc[3 * TRW], shY[HP], bc[3 * TRW], bhY[HP];
+    auto load_cols = [&](uint32_t* c, uint32_t* hY, int cb) {
         const uint32_t oY = col_off_a(cb + dl, kY), oM = col_off_a(cb + dl, kMp), oP = col_off_a(cb - R + dl, kP);
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
-            asm_ld2s(Y[m], Mp[m], oY, oM, dPr, dPr, sIo[m], sIo[m]);
-            asm_ld1s(Pq[m], oP, dPr, sIo[m]);
+            asm_ld2s(c[3 * m], c[3 * m + 1], oY, oM, dPr, dPr, sIo[m], sIo[m]);
+            asm_ld1s(c[3 * m + 2], oP, dPr, sIo[m]);
         }
 #pragma unroll
         for (int i = 0; i < HP; ++i) asm_ld1s(hY[i], wv + NWC * i < NH ? oY : kOOB, dPr, sIh[i]);
@@ -377,7 +382,8 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     auto tie_cols = [&]() {
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
-            asm_tie(sY[m]); asm_tie(sMp[m]); asm_tie(sPq[m]); asm_tie(bY[m]); asm_tie(bMp[m]); asm_tie(bPq[m]);
+            asm_tie(sc[3 * m]); asm_tie(sc[3 * m + 1]); asm_tie(sc[3 * m + 2]);
+            asm_tie(bc[3 * m]); asm_tie(bc[3 * m + 1]); asm_tie(bc[3 * m + 2]);
         }
 #pragma unroll
         for (int i = 0; i < HP; ++i) { asm_tie(shY[i]); asm_tie(bhY[i]); }
@@ -416,16 +422,13 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         tie(cur);
         if constexpr (SLIDE) {
             if (w > w0) {  // move the columns down one lane; lane 63 takes column w + 63 (+ offset)
-#pragma unroll
-                for (int m = 0; m < TRW; ++m) slide3(sY[m], sMp[m], sPq[m], bY[m], bMp[m], bPq[m], lane63);
-#pragma unroll
-                for (int i = 0; i < HP; ++i) slide1(shY[i], bhY[i], lane63);
+                slide_rows<HP>(sc, bc, shY, bhY, lane63);
             }
             // the block for steps w + 1 .. w + 64 (lane i -> step w + 1 + i): columns w + 64 + i (+ offset);
             // issued after this step's reads of the previous block
-            if (((w - w0) & 63) == 0) load_cols(bY, bMp, bPq, bhY, w + 64);
+            if (((w - w0) & 63) == 0) load_cols(bc, bhY, w + 64);
         }
-        issue(w + BDP, nxt);  // past the segment's end: harmless, drained before the wave ends
+        issue(w + BDP, nxt, std::false_type{});  // past the segment's end: harmless, drained before the wave ends
         float* Acur = Abuf + ((w - w0) & 1) * (NY * 64);
         if (lane == 0) {
 #pragma unroll
@@ -442,12 +445,12 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
             const int y = R + yw + m;
-            const float Xf = rbc<m>(F(cur.xo)), Ye = F(SLIDE ? sY[m] : cur.Ye[m]);
+            const float Xf = rbc<m>(F(cur.xo)), Ye = F(SLIDE ? sc[3 * m] : cur.Ye[m]);
             const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, Ye, kEps));
             const float Ae = F(cur.ge[m]) * rSe;
             Acur[y * 64 + lane] = Ae;
             const float V = Ae * F(cur.cv[m]) * rSe;
-            amv[m] = Ae * F(SLIDE ? sMp[m] : cur.mp[m]);
+            amv[m] = Ae * F(SLIDE ? sc[3 * m + 1] : cur.mp[m]);
             bv[m] = V * Ye;
             P[1][m] = shl1_add(P[1][m], Ae * rbc<m>(mco));
             P[2][m] = shl1_add(P[2][m], (V * af) * Xf);
@@ -476,20 +479,23 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             float* rs = ring + (sidx * TRW + m) * 64 + lane;  // V of row m, K steps ago
             HV[m] += v - *rs;
             *rs = v;
-            t1v[m] = (F(SLIDE ? sPq[m] : cur.pq[m]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
+            t1v[m] = (F(SLIDE ? sc[3 * m + 2] : cur.pq[m]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
             P[0][m] = shl1_add(P[0][m], rbc<m>(cxo) * HV[m]);
         });
         sidx = sidx + 1 == K ? 0 : sidx + 1;
-        const float w0r = red16(red32(amv[0], bv[0]), red32(amv[1], bv[1]));
-        const float w1r = red16(red32(amv[2], bv[2]), red32(amv[3], bv[3]));
-        const float w2r = red16(red32(t1v[0], t1v[1]), red32(t1v[2], t1v[3]));
+        // red16(red32(amv0, bv0), red32(amv1, bv1)), ... with the swaps of a level in one asm
+        swap32x6(amv[0], bv[0], amv[1], bv[1], amv[2], bv[2], amv[3], bv[3], t1v[0], t1v[1], t1v[2], t1v[3]);
+        float u0 = amv[0] + bv[0], u1 = amv[1] + bv[1], u2 = amv[2] + bv[2], u3 = amv[3] + bv[3];
+        float u4 = t1v[0] + t1v[1], u5 = t1v[2] + t1v[3];
+        swap16x3(u0, u1, u2, u3, u4, u5);
+        const float w0r = u0 + u1, w1r = u2 + u3, w2r = u4 + u5;
         cbuf[s][qlane] = reduce_tail3(w0r, w1r, w2r, lane);
     };
 
     Ld L[BDP + 1];
-    if constexpr (SLIDE) load_cols(sY, sMp, sPq, shY, w0);  // the first step's columns, all lanes
-    issue(w0, L[0]);
-    if constexpr (BDP == 2) issue(w0 + 1, L[1]);
+    if constexpr (SLIDE) load_cols(sc, shY, w0);  // the first step's columns, all lanes
+    issue(w0, L[0], std::true_type{});
+    if constexpr (BDP == 2) issue(w0 + 1, L[1], std::true_type{});
     for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
         const int nsteps = min(FBC, wend - wfirst);  // FBC = a multiple of BDP + 1: blocks start on L[0]
         const bool fl = wfirst > w0;

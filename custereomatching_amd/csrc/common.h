@@ -146,32 +146,39 @@ __device__ __forceinline__ void asm_ld5s(uint32_t& a0, uint32_t& a1, uint32_t& a
         : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3), "=&v"(a4)
         : "v"(oA), "v"(oB), "v"(oC), "s"(r0), "s"(r1), "s"(r2), "s"(r3), "s"(r4), "s"(sA), "s"(sB));
 }
+// NOP = false drops the `s_nop 4`: only for loads whose SGPR operands no VALU op writes
+// within 5 wait states before them -- custereomatching_amd/hazard_check.py (rule R1) verifies that on
+// the listing at build time for the translation units that use it.
+#define CUSTMA_LD_ASM(NOP, BODY, ...)                       \
+    do {                                                    \
+        if constexpr (NOP)                                  \
+            asm volatile("s_nop 4\n\t" BODY __VA_ARGS__);  \
+        else                                                \
+            asm volatile(BODY __VA_ARGS__);                 \
+    } while (0)
+template <bool NOP = true>
 __device__ __forceinline__ void asm_ld2s(uint32_t& a0, uint32_t& a1, uint32_t oA, uint32_t oB, i32x4 r0, i32x4 r1,
                                          uint32_t sA, uint32_t sB) {
-    asm volatile(
-        "s_nop 4\n\t"
-        "buffer_load_dword %0, %2, %4, %6 offen\n\t"
-        "buffer_load_dword %1, %3, %5, %7 offen"
-        : "=&v"(a0), "=&v"(a1)
-        : "v"(oA), "v"(oB), "s"(r0), "s"(r1), "s"(sA), "s"(sB));
+    CUSTMA_LD_ASM(NOP,
+                  "buffer_load_dword %0, %2, %4, %6 offen\n\t"
+                  "buffer_load_dword %1, %3, %5, %7 offen",
+                  : "=&v"(a0), "=&v"(a1)
+                  : "v"(oA), "v"(oB), "s"(r0), "s"(r1), "s"(sA), "s"(sB));
 }
+template <bool NOP = true>
 __device__ __forceinline__ void asm_ld1s(uint32_t& a0, uint32_t oA, i32x4 r0, uint32_t sA) {
-    asm volatile(
-        "s_nop 4\n\t"
-        "buffer_load_dword %0, %1, %2, %3 offen"
-        : "=&v"(a0)
-        : "v"(oA), "s"(r0), "s"(sA));
+    CUSTMA_LD_ASM(NOP, "buffer_load_dword %0, %1, %2, %3 offen", : "=&v"(a0) : "v"(oA), "s"(r0), "s"(sA));
 }
+template <bool NOP = true>
 __device__ __forceinline__ void asm_ld4(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t oA,
                                         uint32_t oB, uint32_t oC, uint32_t oD, i32x4 r0, i32x4 r1, i32x4 r2) {
-    asm volatile(
-        "s_nop 4\n\t"
-        "buffer_load_dword %0, %4, %8, 0 offen\n\t"
-        "buffer_load_dword %1, %5, %8, 0 offen\n\t"
-        "buffer_load_dword %2, %6, %9, 0 offen\n\t"
-        "buffer_load_dword %3, %7, %10, 0 offen"
-        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
-        : "v"(oA), "v"(oB), "v"(oC), "v"(oD), "s"(r0), "s"(r1), "s"(r2));
+    CUSTMA_LD_ASM(NOP,
+                  "buffer_load_dword %0, %4, %8, 0 offen\n\t"
+                  "buffer_load_dword %1, %5, %8, 0 offen\n\t"
+                  "buffer_load_dword %2, %6, %9, 0 offen\n\t"
+                  "buffer_load_dword %3, %7, %10, 0 offen",
+                  : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+                  : "v"(oA), "v"(oB), "v"(oC), "v"(oD), "s"(r0), "s"(r1), "s"(r2));
 }
 // Image-row groups for the forward sweep: 8 image loads (projector enter/leave x 2 halves,
 // camera enter/leave x 2 halves) / 6 statistics loads, rows selected by SGPR soffsets.

@@ -18,34 +18,178 @@ __device__ __forceinline__ float rbc(float a) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0x150 + L, 0xf, 0xf,
                                                                  true));
 }
-// Sliding column registers (backward sweep): v moves down one lane (lane l <- v[l + 1],
-// wave_shl:1) and its lane 63 takes lane 63 of the block register b, which first rotates
+// Sliding column registers (backward sweep): each v moves down one lane (lane l <- v[l + 1],
+// wave_shl:1) and its lane 63 takes lane 63 of its block register b, which first rotates
 // down one lane (wave_rol:1: lane l <- b[(l + 1) & 63]).  After its i-th rotation since it
 // was loaded, b's lane 63 holds the block's element i - 1, so a block loaded once feeds 64
-// steps at two VALU ops per register and step.  `s_nop 1`: a DPP source written by the
-// previous VALU op needs 2 wait states; VCC (the lane-63 select) is written by SALU.
-__device__ __forceinline__ void slide3(uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& b0, uint32_t& b1,
-                                       uint32_t& b2, uint64_t lane63) {
+// steps at two VALU ops per register and step.  The 12 own-row registers and the HP halo
+// registers go through one asm block (VCC, the lane-63 select, set once by SALU).  No
+// `s_nop`: the DPP sources were last written a step earlier; custereomatching_amd/hazard_check.py checks
+// that on the listing at build time (rule R2: VALU write -> DPP read, 2 wait states).
+template <int HP>
+__device__ __forceinline__ void slide_rows(uint32_t (&v)[12], uint32_t (&b)[12], uint32_t (&hv)[HP],
+                                           uint32_t (&hb)[HP], uint64_t lane63);
+template <>
+__device__ __forceinline__ void slide_rows<1>(uint32_t (&v)[12], uint32_t (&b)[12], uint32_t (&hv)[1], uint32_t (&hb)[1],
+                                                uint64_t lane63) {
     asm volatile(
-        "s_mov_b64 vcc, %6\n\t"
-        "s_nop 1\n\t"
-        "v_mov_b32_dpp %3, %3 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b32_dpp %4, %4 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b32_dpp %5, %5 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_dpp %0, %0, %3, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
-        "v_cndmask_b32_dpp %1, %1, %4, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
-        "v_cndmask_b32_dpp %2, %2, %5, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
-        : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(b0), "+v"(b1), "+v"(b2)
+        "s_mov_b64 vcc, %26\n\t"
+        "v_mov_b32_dpp %13, %13 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %14, %14 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %15, %15 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %16, %16 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %17, %17 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %18, %18 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %19, %19 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %20, %20 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %21, %21 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %22, %22 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %23, %23 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %24, %24 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %25, %25 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %0, %0, %13, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %1, %1, %14, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %2, %2, %15, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %3, %3, %16, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %4, %4, %17, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %5, %5, %18, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %6, %6, %19, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %7, %7, %20, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %8, %8, %21, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %9, %9, %22, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %10, %10, %23, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %11, %11, %24, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %12, %12, %25, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+        : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+          "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(hv[0]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]),
+          "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]), "+v"(b[8]), "+v"(b[9]), "+v"(b[10]),
+          "+v"(b[11]), "+v"(hb[0])
         : "s"(lane63)
         : "vcc");
 }
-__device__ __forceinline__ void slide1(uint32_t& v, uint32_t& b, uint64_t lane63) {
+template <>
+__device__ __forceinline__ void slide_rows<2>(uint32_t (&v)[12], uint32_t (&b)[12], uint32_t (&hv)[2], uint32_t (&hb)[2],
+                                                uint64_t lane63) {
     asm volatile(
-        "s_mov_b64 vcc, %2\n\t"
-        "s_nop 1\n\t"
-        "v_mov_b32_dpp %1, %1 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_cndmask_b32_dpp %0, %0, %1, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
-        : "+v"(v), "+v"(b)
+        "s_mov_b64 vcc, %28\n\t"
+        "v_mov_b32_dpp %14, %14 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %15, %15 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %16, %16 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %17, %17 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %18, %18 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %19, %19 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %20, %20 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %21, %21 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %22, %22 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %23, %23 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %24, %24 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %25, %25 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %26, %26 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %27, %27 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %0, %0, %14, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %1, %1, %15, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %2, %2, %16, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %3, %3, %17, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %4, %4, %18, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %5, %5, %19, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %6, %6, %20, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %7, %7, %21, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %8, %8, %22, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %9, %9, %23, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %10, %10, %24, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %11, %11, %25, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %12, %12, %26, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %13, %13, %27, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+        : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+          "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(hv[0]), "+v"(hv[1]), "+v"(b[0]), "+v"(b[1]),
+          "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]), "+v"(b[8]), "+v"(b[9]),
+          "+v"(b[10]), "+v"(b[11]), "+v"(hb[0]), "+v"(hb[1])
+        : "s"(lane63)
+        : "vcc");
+}
+template <>
+__device__ __forceinline__ void slide_rows<3>(uint32_t (&v)[12], uint32_t (&b)[12], uint32_t (&hv)[3], uint32_t (&hb)[3],
+                                                uint64_t lane63) {
+    asm volatile(
+        "s_mov_b64 vcc, %30\n\t"
+        "v_mov_b32_dpp %15, %15 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %16, %16 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %17, %17 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %18, %18 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %19, %19 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %20, %20 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %21, %21 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %22, %22 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %23, %23 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %24, %24 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %25, %25 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %26, %26 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %27, %27 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %28, %28 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %29, %29 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %0, %0, %15, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %1, %1, %16, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %2, %2, %17, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %3, %3, %18, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %4, %4, %19, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %5, %5, %20, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %6, %6, %21, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %7, %7, %22, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %8, %8, %23, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %9, %9, %24, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %10, %10, %25, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %11, %11, %26, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %12, %12, %27, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %13, %13, %28, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %14, %14, %29, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+        : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+          "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]), "+v"(b[0]),
+          "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]), "+v"(b[8]),
+          "+v"(b[9]), "+v"(b[10]), "+v"(b[11]), "+v"(hb[0]), "+v"(hb[1]), "+v"(hb[2])
+        : "s"(lane63)
+        : "vcc");
+}
+template <>
+__device__ __forceinline__ void slide_rows<4>(uint32_t (&v)[12], uint32_t (&b)[12], uint32_t (&hv)[4], uint32_t (&hb)[4],
+                                                uint64_t lane63) {
+    asm volatile(
+        "s_mov_b64 vcc, %32\n\t"
+        "v_mov_b32_dpp %16, %16 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %17, %17 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %18, %18 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %19, %19 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %20, %20 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %21, %21 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %22, %22 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %23, %23 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %24, %24 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %25, %25 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %26, %26 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %27, %27 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %28, %28 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %29, %29 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %30, %30 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %31, %31 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %0, %0, %16, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %1, %1, %17, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %2, %2, %18, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %3, %3, %19, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %4, %4, %20, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %5, %5, %21, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %6, %6, %22, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %7, %7, %23, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %8, %8, %24, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %9, %9, %25, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %10, %10, %26, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %11, %11, %27, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %12, %12, %28, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %13, %13, %29, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %14, %14, %30, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "v_cndmask_b32_dpp %15, %15, %31, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+        : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+          "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]), "+v"(hv[3]),
+          "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]),
+          "+v"(b[8]), "+v"(b[9]), "+v"(b[10]), "+v"(b[11]), "+v"(hb[0]), "+v"(hb[1]), "+v"(hb[2]), "+v"(hb[3])
         : "s"(lane63)
         : "vcc");
 }
@@ -100,6 +244,29 @@ __device__ __forceinline__ float reduce48(float (&v)[48], int lane) {
     const float z0 = pair_level<kQuad3210, 2>(y[0], y[1], lane);
     const float z1 = y[2] + dpp<kQuad3210>(y[2]);
     return pair_level<kQuad1032, 1>(z0, z1, lane);
+}
+// A reduction level's swaps in one asm: one `s_nop 1` (the inputs may be fresh VALU results)
+// instead of two v_nop per swap.
+__device__ __forceinline__ void swap32x6(float& a0, float& b0, float& a1, float& b1, float& a2, float& b2, float& a3,
+                                         float& b3, float& a4, float& b4, float& a5, float& b5) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_permlane32_swap_b32 %0, %1\n\t"
+        "v_permlane32_swap_b32 %2, %3\n\t"
+        "v_permlane32_swap_b32 %4, %5\n\t"
+        "v_permlane32_swap_b32 %6, %7\n\t"
+        "v_permlane32_swap_b32 %8, %9\n\t"
+        "v_permlane32_swap_b32 %10, %11"
+        : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3), "+v"(a4), "+v"(b4),
+          "+v"(a5), "+v"(b5));
+}
+__device__ __forceinline__ void swap16x3(float& a0, float& b0, float& a1, float& b1, float& a2, float& b2) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_permlane16_swap_b32 %0, %1\n\t"
+        "v_permlane16_swap_b32 %2, %3\n\t"
+        "v_permlane16_swap_b32 %4, %5"
+        : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2));
 }
 // Pair reductions for values produced one at a time: (a, b) -> one register holding
 // a's pair sums in the low half (or even rows) and b's in the other.
