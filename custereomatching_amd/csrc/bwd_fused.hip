@@ -175,10 +175,20 @@ constexpr int BDP = CUSTMA_BWD_DEPTH;  // steps of loads in flight (1 or 2)
 // lane per step (DPP wave_shl:1) and only lane 63 takes a new column, read from a register
 // loaded once per 64 steps -- instead of a 64-lane load of each per step (those image rows
 // do not stay in L2 beside the gradient stream: ~half of the kernel's L2 misses).
-constexpr bool SLIDE = CUSTMA_BWD_SLIDE && BDP == 1;
+constexpr bool SLIDE = CUSTMA_BWD_SLIDE;
 // steps per flush (small buffers: 3 workgroups per CU at k = 9); a multiple of BDP + 1, so
 // every flush block starts on load buffer 0
-constexpr int FBC = BDP == 2 ? 6 : 8;
+#ifndef CUSTMA_BWD_FBC
+#define CUSTMA_BWD_FBC (BDP == 2 ? 6 : 8)
+#endif
+constexpr int FBC = CUSTMA_BWD_FBC;
+static_assert(FBC % (BDP + 1) == 0 && FBC <= 16, "flush blocks start on load buffer 0; 4 FBC lanes");
+// A rows of the unit: double-buffered (one barrier per step) or single (a second barrier
+// before the next step's writes; 6.5 KB less LDS at k = 11)
+#ifndef CUSTMA_BWD_ABUF
+#define CUSTMA_BWD_ABUF 2
+#endif
+constexpr int NAB = CUSTMA_BWD_ABUF;
 
 // Finish 3 registers (each already summed over the 4 lanes {l, l+16, l+32, l+48}, one
 // value per 16-lane row): afterwards every lane holds the full 64-lane sum of one of the 12.
@@ -264,8 +274,10 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     auto part_rsrc = [&](int t) {
         return make_rsrc(a.part + ((size_t)t * a.S + slot) * plane + (size_t)(y0 + yw) * g.W, prow_bytes);
     };
+    // loads per issue() (asm_ld2s / asm_ld1s / asm_ld4), per thread
+    constexpr int NLD = (SLIDE ? TRW * 2 + (HPW > 0 ? HPW : 1) : TRW * 5 + (HPW > 0 ? HPW : 1) * 2) + 4;
     auto flush = [&](int wfirst, int nsteps) {
-        if constexpr (BDP == 2) asm_vmcnt<TRW * 5 + (HPW > 0 ? HPW : 1) * 2 + 4>();  // all but the newest issue
+        if constexpr (BDP == 2) asm_vmcnt<NLD>();  // all but the newest issue
         int ln = lane;
         asm volatile("" : "+v"(ln));
         // lanes 0..4 FBC-1: step jcol, own row m (the rest idle)
@@ -342,7 +354,11 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         constexpr bool NOP = decltype(nop_)::value;
         const int xb = w - R;
         const bool ve = w >= lwlo && w < lwhi;
+#ifdef CUSTMA_ABL_BWD_NOMEM  // ablation (timing only): no gradient / volume traffic
+        const uint32_t oGe = kOOB + 0 * ve;
+#else
         const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
+#endif
         const uint32_t oYe = col_off_a(w + dl, kY), oMe = col_off_a(w + dl, kMp), oPq = col_off_a(xb + dl, kP);
         if constexpr (SLIDE) {
 #pragma unroll
@@ -406,15 +422,16 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
 
     int sidx = 0;  // ring slot of the current step (step count mod K)
-    // loads per issue() (asm_ld5s / asm_ld2s / asm_ld4) and stores per flush(), per thread
-    constexpr int NL = (SLIDE ? TRW * 2 + HP : TRW * 5 + HP * 2) + 4, SF = 6;
+    // loads per issue() and stores per flush(), per thread
+    constexpr int NL = NLD, SF = 6;
     static_assert(NL + SF <= 63, "vmcnt holds the pipeline");
     // cur was issued BDP steps ago; issued since: the later steps' loads, and a flush's SF
     // stores after step s = FBC-1 of the previous block (flush() itself waits until only
     // the newest issue is in flight: at s = 0 of a block after a flush cur has landed)
     auto step = [&](Ld& cur, Ld& nxt, int w, int s, bool flushed) {
         if constexpr (BDP == 2) {
-            if (!flushed || s >= 2) asm_vmcnt<NL>();
+            // SLIDE: a column block issued at s = 0 (after the flush's stores) feeds step 1
+            if (!flushed || s >= 2 || (SLIDE && s == 1)) asm_vmcnt<NL>();
             else if (s == 1) asm_vmcnt<NL + SF>();
         } else {
             asm_vmcnt<0>();
@@ -429,7 +446,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             if (((w - w0) & 63) == 0) load_cols(bc, bhY, w + 64);
         }
         issue(w + BDP, nxt, std::false_type{});  // past the segment's end: harmless, drained before the wave ends
-        float* Acur = Abuf + ((w - w0) & 1) * (NY * 64);
+        float* Acur = Abuf + (NAB == 2 ? ((w - w0) & 1) * (NY * 64) : 0);
         if (lane == 0) {
 #pragma unroll
             for (int t = 0; t < 3; ++t)
@@ -442,6 +459,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         // ---- own rows: A, and the per-voxel terms (unit rows R + yw .. R + yw + 3); the
         // row's camera values come from quad slot m of the row-replicated registers ----
         float amv[TRW], bv[TRW];
+        if constexpr (NAB == 1) __syncthreads();  // every wave has read the previous step's A rows
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
             const int y = R + yw + m;
@@ -533,8 +551,13 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     }
 }
 
+#ifdef CUSTMA_BWD_WPE
+#define CUSTMA_BWD_OCC __attribute__((amdgpu_waves_per_eu(CUSTMA_BWD_WPE)))
+#else
+#define CUSTMA_BWD_OCC
+#endif
 template <int K>
-__global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
+__global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, BwdArgs a) {
     // XCD x owns row groups [x nRGx, (x+1) nRGx) (their halo rows are read on one XCD).
     // A wave's 256-byte gradient / volume row segment spans three 128-byte lines whose outer
     // parts the neighbouring diagonal chunk's workgroup reads at the same step; the order
@@ -564,7 +587,7 @@ __global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
     }
     if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
     constexpr int NY = TRB + 2 * (K / 2);
-    __shared__ __attribute__((aligned(16))) float Abuf[2 * NY * 64];
+    __shared__ __attribute__((aligned(16))) float Abuf[NAB * NY * 64];
     __shared__ __attribute__((aligned(16))) float ring[NWC * K * TRW * 64];
     __shared__ __attribute__((aligned(16))) float cbuf[NWC][FBC][12];
     __shared__ __attribute__((aligned(16))) float pbuf[NWC][FBC][12];

@@ -32,63 +32,67 @@ constexpr int TW = 16;  // camera (own-image) columns per workgroup
 //
 // Hazard: a DPP source VGPR written by a VALU instruction needs 2 wait states before the
 // DPP read (gfx9 "VALU write VGPR -> DPP read").  The compiler cannot see the DPP inside
-// the asm, so every asm block below starts with `s_nop 1`; the batched forms amortise it
-// over several FMAs.
-template <int L>
+// the asm, so with NOP = true every asm block below starts with `s_nop 1`.  NOP = false
+// drops it where the operands are step constants; custereomatching_amd/hazard_check.py
+// verifies the emitted listing of such translation units at build time (rule R2).
+#define CUSTMA_DPP_ASM(NOP, BODY, ...)                      \
+    do {                                                    \
+        if constexpr (NOP)                                  \
+            asm("s_nop 1\n\t" BODY __VA_ARGS__);            \
+        else                                                \
+            asm(BODY __VA_ARGS__);                          \
+    } while (0)
+template <int L, bool NOP = true>
 __device__ __forceinline__ void fmac_bc64(double& acc, double a, double b) {
-    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-        : "+v"(acc) : "v"(a), "v"(b), "i"(L));
+    CUSTMA_DPP_ASM(NOP, "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf",
+                   : "+v"(acc) : "v"(a), "v"(b), "i"(L));
 }
-template <int L>
+template <int L, bool NOP = true>
 __device__ __forceinline__ void fmac_bc32(float& acc, float a, float b) {
-    asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-        : "+v"(acc) : "v"(a), "v"(b), "i"(L));
+    CUSTMA_DPP_ASM(NOP, "v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf",
+                   : "+v"(acc) : "v"(a), "v"(b), "i"(L));
 }
 // acc[i] += bcast(a, lane L+i) * pa[i] + bcast(b, lane L+i) * pb[i] for i < 4 (in that order)
-template <int L>
+template <int L, bool NOP = true>
 __device__ __forceinline__ void fmac2_bc64_x4(double& c0, double& c1, double& c2, double& c3, double a, double b,
                                               double pa0, double pa1, double pa2, double pa3, double pb0,
                                               double pb1, double pb2, double pb3) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %4, %6 row_newbcast:%14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %4, %7 row_newbcast:%15 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %4, %8 row_newbcast:%16 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %4, %9 row_newbcast:%17 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %5, %10 row_newbcast:%14 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %5, %11 row_newbcast:%15 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %5, %12 row_newbcast:%16 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %5, %13 row_newbcast:%17 row_mask:0xf bank_mask:0xf"
-        : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
-        : "v"(a), "v"(b), "v"(pa0), "v"(pa1), "v"(pa2), "v"(pa3), "v"(pb0), "v"(pb1), "v"(pb2), "v"(pb3),
-          "i"(L), "i"(L + 1), "i"(L + 2), "i"(L + 3));
+    CUSTMA_DPP_ASM(NOP,
+                   "v_fmac_f64_dpp %0, %4, %6 row_newbcast:%14 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %1, %4, %7 row_newbcast:%15 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %2, %4, %8 row_newbcast:%16 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %3, %4, %9 row_newbcast:%17 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %0, %5, %10 row_newbcast:%14 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %1, %5, %11 row_newbcast:%15 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %2, %5, %12 row_newbcast:%16 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %3, %5, %13 row_newbcast:%17 row_mask:0xf bank_mask:0xf",
+                   : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+                   : "v"(a), "v"(b), "v"(pa0), "v"(pa1), "v"(pa2), "v"(pa3), "v"(pb0), "v"(pb1), "v"(pb2),
+                     "v"(pb3), "i"(L), "i"(L + 1), "i"(L + 2), "i"(L + 3));
 }
-template <int L>
+template <int L, bool NOP = true>
 __device__ __forceinline__ void fmac2_bc64_x2(double& c0, double& c1, double a, double b, double pa0, double pa1,
                                               double pb0, double pb1) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %2, %4 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %2, %5 row_newbcast:%9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %3, %6 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %3, %7 row_newbcast:%9 row_mask:0xf bank_mask:0xf"
-        : "+v"(c0), "+v"(c1)
-        : "v"(a), "v"(b), "v"(pa0), "v"(pa1), "v"(pb0), "v"(pb1), "i"(L), "i"(L + 1));
+    CUSTMA_DPP_ASM(NOP,
+                   "v_fmac_f64_dpp %0, %2, %4 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %1, %2, %5 row_newbcast:%9 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %0, %3, %6 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
+                   "v_fmac_f64_dpp %1, %3, %7 row_newbcast:%9 row_mask:0xf bank_mask:0xf",
+                   : "+v"(c0), "+v"(c1)
+                   : "v"(a), "v"(b), "v"(pa0), "v"(pa1), "v"(pb0), "v"(pb1), "i"(L), "i"(L + 1));
 }
-// e += bcast(nb, lane L) * mv;  den2 += bcast(uq, lane L) * qv  (the finalisation's two DPP FMAs)
-// NOP = false: the caller guarantees nb and uq were not written by the previous two VALU
-// instructions (e.g. every call after the first of a step, nb / uq being step constants).
-template <int L, bool NOP = true>
-__device__ __forceinline__ void fin_bc(double& e, float& den2, double nb, double mv, float uq, float qv) {
-    if constexpr (NOP)
-        asm("s_nop 1\n\t"
-            "v_fmac_f64_dpp %0, %2, %3 row_newbcast:%6 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %1, %4, %5 row_newbcast:%6 row_mask:0xf bank_mask:0xf"
-            : "+v"(e), "+v"(den2)
-            : "v"(nb), "v"(mv), "v"(uq), "v"(qv), "i"(L));
-    else
-        asm("v_fmac_f64_dpp %0, %2, %3 row_newbcast:%6 row_mask:0xf bank_mask:0xf\n\t"
-            "v_fmac_f32_dpp %1, %4, %5 row_newbcast:%6 row_mask:0xf bank_mask:0xf"
-            : "+v"(e), "+v"(den2)
-            : "v"(nb), "v"(mv), "v"(uq), "v"(qv), "i"(L));
+// e = s + bcast(nb, lane L) * mv;  den2 = eps + bcast(uq, lane L) * qv  (the finalisation's
+// two DPP FMAs).  The two initialising moves go first inside the asm: they are the 2 wait
+// states a DPP source written by the previous VALU op needs, so no `s_nop` is spent.
+template <int L>
+__device__ __forceinline__ void fin_bc(double& e, float& den2, double s, double nb, double mv, float uq, float qv) {
+    static_assert(kEps == 1e-8f, "the asm's literal is kEps");
+    asm("v_mov_b64 %0, %6\n\t"
+        "v_mov_b32 %1, 0x322bcc77\n\t"
+        "v_fmac_f64_dpp %0, %2, %3 row_newbcast:%7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %4, %5 row_newbcast:%7 row_mask:0xf bank_mask:0xf"
+        : "=&v"(e), "=&v"(den2)
+        : "v"(nb), "v"(mv), "v"(uq), "v"(qv), "v"(s), "i"(L));
 }
 
 // Kernel sizes with a compile-time sweep instantiation (register-resident

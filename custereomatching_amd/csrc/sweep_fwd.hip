@@ -308,11 +308,11 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         for (int m = 0; m < TWT; ++m) v[m] = *(const float*)(tile + voff[m] + 4 * (m * stgA + stgB));
 #ifndef CUSTMA_ABL_NOSTORE  // ablation builds only (scripts/build_ablations.py)
 #pragma unroll
-        for (int m = 0; m < TWT; ++m) st_buf(v[m], rOut, voff[m]);
+        for (int m = 0; m < TWT; ++m) st_vol(v[m], rOut, voff[m]);
 #else
 #pragma unroll
         for (int m = 0; m < TWT; ++m)
-            if (v[m] == 1234.5f) st_buf(v[m], rOut, voff[m]);
+            if (v[m] == 1234.5f) st_vol(v[m], rOut, voff[m]);
 #endif
     };
 
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 if constexpr (ARGMAX) {
                     srow[m * NL] = (m >= m_lo && m < m_hi) ? c : -FLT_MAX;
                 } else if constexpr (DIRECT) {
-                    if (h >= h0) st_buf(c, rOutD, dvoff[m]);
+                    if (h >= h0) st_vol(c, rOutD, dvoff[m]);
                 } else {
                     srow[m * NL] = c;
                 }

@@ -45,6 +45,16 @@ typedef __attribute__((address_space(3))) volatile double lds_vd;
 typedef __attribute__((address_space(3))) volatile float lds_vf;
 
 constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
+// The row update's DPP FMAs keep their `s_nop 1` only where a camera operand may have just
+// been converted (the first group of each 16-column half); hazard_check.py checks the
+// listing at build time.  CUSTMA_DPP_NOP=1 puts them back everywhere (benchmarking)
+#ifndef CUSTMA_DPP_NOP
+#define CUSTMA_DPP_NOP 0
+#endif
+constexpr bool kDppNop = CUSTMA_DPP_NOP != 0;
+#ifndef CUSTMA_FWD_PF
+#define CUSTMA_FWD_PF 2  // outputs whose statistics are read ahead
+#endif
 
 // REM: this wave (window layout, last chunk, (D+1) % 64 == 1) also computes the single
 // remainder diagonal d0 + 64 = D: lane x < 16 + 2r keeps its column sum, the horizontal box
@@ -232,15 +242,15 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 const double* qa = pa[bb & 1];
                 const double* qb = pb[bb & 1];
                 if constexpr (nb_ == 4) {
-                    fmac2_bc64_x4<(x0 & 15)>(col[x0], col[x0 + 1], col[x0 + 2], col[x0 + 3], a, b, qa[0], qa[1],
+                    fmac2_bc64_x4<(x0 & 15), kDppNop || x0 == 0 || x0 == 16>(col[x0], col[x0 + 1], col[x0 + 2], col[x0 + 3], a, b, qa[0], qa[1],
                                              qa[2], qa[3], qb[0], qb[1], qb[2], qb[3]);
                 } else if constexpr (nb_ == 2) {
-                    fmac2_bc64_x2<(x0 & 15)>(col[x0], col[x0 + 1], a, b, qa[0], qa[1], qb[0], qb[1]);
+                    fmac2_bc64_x2<(x0 & 15), kDppNop || x0 == 0 || x0 == 16>(col[x0], col[x0 + 1], a, b, qa[0], qa[1], qb[0], qb[1]);
                 } else {
                     Unroll<0, nb_>::run([&](auto ic) {
                         constexpr int i = decltype(ic)::value, x = x0 + i;
-                        fmac_bc64<(x & 15)>(col[x], a, qa[i]);
-                        fmac_bc64<(x & 15)>(col[x], b, qb[i]);
+                        fmac_bc64<(x & 15), kDppNop || x0 == 0 || x0 == 16>(col[x], a, qa[i]);
+                        fmac_bc64<(x & 15), kDppNop || x0 == 0 || x0 == 16>(col[x], b, qb[i]);
                     });
                 }
             });
@@ -258,8 +268,20 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
 #pragma unroll
             for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
-            const lds_vd* mrow = (const lds_vd*)(sM + l);
-            const lds_vf* qrow = (const lds_vf*)(sQ + l);
+            // the projector mean / moment of output m, read PF outputs ahead (plain reads, issued
+            // in program order before the stage writes of the outputs in between)
+            typedef __attribute__((address_space(3))) const double lds_d;
+            typedef __attribute__((address_space(3))) const float lds_f;
+            const lds_d* mrow = (const lds_d*)(sM + l);
+            const lds_f* qrow = (const lds_f*)(sQ + l);
+            constexpr int PF = CUSTMA_FWD_PF;
+            double mq[PF];
+            float qq[PF];
+            Unroll<0, PF>::run([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                mq[i] = mrow[i];
+                qq[i] = qrow[i];
+            });
             lds_vf* sb = (lds_vf*)(stage + (t & 1) * TW * DO);  // STAGED: this step's buffer
             const bool dv = d0 + l <= g.D;
             // every lane of the chunk valid (all but a partial last chunk): unmasked stage writes,
@@ -270,10 +292,16 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             Unroll<0, TW>::run([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
                 if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
-                double e = s;
-                float den2 = kEps;
+                double e;
+                float den2;
+                const double mv = mq[m % PF];
+                const float qv = qq[m % PF];
+                if constexpr (m + PF < TW) {
+                    mq[m % PF] = mrow[m + PF];
+                    qq[m % PF] = qrow[m + PF];
+                }
                 // E + eps = S + eps - box_c * mean_p;  ex2 * ey2 + eps
-                fin_bc<m>(e, den2, nb, mrow[m], uq, qrow[m]);
+                fin_bc<m>(e, den2, s, nb, mv, uq, qv);
 #ifdef CUSTMA_ABL_NOOUT
                 const float c = (float)m;
 #else

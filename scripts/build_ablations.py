@@ -17,8 +17,18 @@ VARIANTS = {
     "storeonly": (["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT"], FWD),
     "nowait": (["CUSTMA_ABL_NOWAIT"], FWD), "stats7": (["CUSTMA_ABL_STATS7"], FWD),
     "early": (["CUSTMA_TILE_EARLY"], FWD),
+    # volume-store cache policy (gfx950 aux bits: 1 sc0, 2 nt, 16 sc1)
+    "st_plain": (["CUSTMA_STORE_AUX=0"], FWD), "st_sc1": (["CUSTMA_STORE_AUX=16"], FWD),
+    "st_ntsc1": (["CUSTMA_STORE_AUX=18"], FWD),
     # backward unit height / block order (bwd_fused.hip)
     "r32": (["CUSTMA_BWD_ROWS=32"], BWD),  # block order: CUSTMA_BWD_ORDER=1|2 at run time
+    # backward LDS: single A buffer + 4-step flushes (k = 11: 61 -> 52 KB, 3 workgroups per CU)
+    "ab1": (["CUSTMA_BWD_ABUF=1", "CUSTMA_BWD_FBC=4"], BWD),
+    "ab1f8": (["CUSTMA_BWD_ABUF=1"], BWD),
+    # backward loads two steps ahead (sliding columns kept)
+    "bdp2": (["CUSTMA_BWD_DEPTH=2"], BWD),
+    "bwdnomem": (["CUSTMA_ABL_BWD_NOMEM"], BWD),  # timing only: gradient / volume loads out of range
+    "bdp2ab1": (["CUSTMA_BWD_DEPTH=2", "CUSTMA_BWD_ABUF=1", "CUSTMA_BWD_FBC=6"], BWD),
 }
 for n in (sys.argv[1:] or VARIANTS):
     d, only = VARIANTS[n]
