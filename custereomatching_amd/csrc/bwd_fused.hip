@@ -428,6 +428,19 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     // cur was issued BDP steps ago; issued since: the later steps' loads, and a flush's SF
     // stores after step s = FBC-1 of the previous block (flush() itself waits until only
     // the newest issue is in flight: at s = 0 of a block after a flush cur has landed)
+    // A step's 12 camera sums are reduced across the lanes during the NEXT step's A phase
+    // (before its barrier), where the reduction's dependency chain overlaps independent
+    // work; the block's last step is reduced before the flush (drain()).
+    float rA[TRW], rB[TRW], rT[TRW];
+    auto reduce_to = [&](int slot) {
+        // red16(red32(amv0, bv0), red32(amv1, bv1)), ... with the swaps of a level in one asm
+        swap32x6(rA[0], rB[0], rA[1], rB[1], rA[2], rB[2], rA[3], rB[3], rT[0], rT[1], rT[2], rT[3]);
+        float u0 = rA[0] + rB[0], u1 = rA[1] + rB[1], u2 = rA[2] + rB[2], u3 = rA[3] + rB[3];
+        float u4 = rT[0] + rT[1], u5 = rT[2] + rT[3];
+        swap16x3(u0, u1, u2, u3, u4, u5);
+        const float w0r = u0 + u1, w1r = u2 + u3, w2r = u4 + u5;
+        cbuf[slot][qlane] = reduce_tail3(w0r, w1r, w2r, lane);
+    };
     auto step = [&](Ld& cur, Ld& nxt, int w, int s, bool flushed) {
         if constexpr (BDP == 2) {
             // SLIDE: a column block issued at s = 0 (after the flush's stores) feeds step 1
@@ -447,6 +460,11 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         }
         issue(w + BDP, nxt, std::false_type{});  // past the segment's end: harmless, drained before the wave ends
         float* Acur = Abuf + (NAB == 2 ? ((w - w0) & 1) * (NY * 64) : 0);
+        // this wave's ring slot of the step (V of its rows K steps ago): wave-private, so read
+        // ahead of the barrier
+        float rsv[TRW];
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) rsv[m] = ring[(sidx * TRW + m) * 64 + lane];
         if (lane == 0) {
 #pragma unroll
             for (int t = 0; t < 3; ++t)
@@ -482,6 +500,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
                                                          __builtin_fmaf(rbc<i>(F(cur.xh)), F(SLIDE ? shY[i] : cur.hY[i]), kEps));
             }
         });
+        if (s > 0) reduce_to(s - 1);
         __syncthreads();  // the unit's A rows of this step are published
         // ---- vertical k-row sums of own rows, horizontal slide through the ring ----
         float col[TRW + 2 * R];
@@ -494,20 +513,18 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
             if (m > 0) v = (v + col[m + 2 * R]) - col[m - 1];
-            float* rs = ring + (sidx * TRW + m) * 64 + lane;  // V of row m, K steps ago
-            HV[m] += v - *rs;
-            *rs = v;
+            HV[m] += v - rsv[m];
+            ring[(sidx * TRW + m) * 64 + lane] = v;
             t1v[m] = (F(SLIDE ? sc[3 * m + 2] : cur.pq[m]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
             P[0][m] = shl1_add(P[0][m], rbc<m>(cxo) * HV[m]);
         });
         sidx = sidx + 1 == K ? 0 : sidx + 1;
-        // red16(red32(amv0, bv0), red32(amv1, bv1)), ... with the swaps of a level in one asm
-        swap32x6(amv[0], bv[0], amv[1], bv[1], amv[2], bv[2], amv[3], bv[3], t1v[0], t1v[1], t1v[2], t1v[3]);
-        float u0 = amv[0] + bv[0], u1 = amv[1] + bv[1], u2 = amv[2] + bv[2], u3 = amv[3] + bv[3];
-        float u4 = t1v[0] + t1v[1], u5 = t1v[2] + t1v[3];
-        swap16x3(u0, u1, u2, u3, u4, u5);
-        const float w0r = u0 + u1, w1r = u2 + u3, w2r = u4 + u5;
-        cbuf[s][qlane] = reduce_tail3(w0r, w1r, w2r, lane);
+#pragma unroll
+        for (int m = 0; m < TRW; ++m) {
+            rA[m] = amv[m];
+            rB[m] = bv[m];
+            rT[m] = t1v[m];
+        }
     };
 
     Ld L[BDP + 1];
@@ -532,6 +549,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
                 step(L[1], L[0], wfirst + s + 1, s + 1, fl);
             }
         }
+        reduce_to(nsteps - 1);
         flush(wfirst, nsteps);
     }
     // The last steps' prefetches are still in flight: keep their registers live (the compiler
