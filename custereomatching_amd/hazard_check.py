@@ -119,14 +119,20 @@ def blocks_of(lines, a, b):
             labels[m.group(1)] = len(blocks)
             blocks.append(cur)
             continue
+        if re.match(r"^; %bb\.\d+:", s):  # a fall-through block without a label
+            cur = None
+            continue
         if not s or s.startswith((";", ".")):
             continue
-        if cur is None:
-            cur = {"label": "<entry>", "ins": []}
-            blocks.append(cur)
         s = s.split(";")[0].strip()
-        if s:
-            cur["ins"].append(Ins(s, asm, ln + 1))
+        if not s:
+            continue
+        if cur is None:
+            cur = {"label": f"<bb@{ln + 1}>", "ins": []}
+            blocks.append(cur)
+        cur["ins"].append(Ins(s, asm, ln + 1))
+        if cur["ins"][-1].op.startswith(("s_branch", "s_cbranch", "s_endpgm", "s_setpc")):
+            cur = None  # a branch ends its block: what follows is the fall-through block
     succ = []
     for bi, bl in enumerate(blocks):
         nxt = []

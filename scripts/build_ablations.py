@@ -28,6 +28,12 @@ VARIANTS = {
     # backward loads two steps ahead (sliding columns kept)
     "bdp2": (["CUSTMA_BWD_DEPTH=2"], BWD),
     "bwdnomem": (["CUSTMA_ABL_BWD_NOMEM"], BWD),  # timing only: gradient / volume loads out of range
+    # knockouts (timing only, wrong results): no lane reductions / no column slide / no halo A rows
+    "ko_red": (["CUSTMA_ABL_KO_RED"], BWD), "ko_slide": (["CUSTMA_ABL_KO_SLIDE"], BWD),
+    "ko_halo": (["CUSTMA_ABL_KO_HALO"], BWD), "ko_bar": (["CUSTMA_ABL_KO_BAR"], BWD),
+    "ko_col": (["CUSTMA_ABL_KO_COL"], BWD),
+    "ko_nomem_bar": (["CUSTMA_ABL_BWD_NOMEM", "CUSTMA_ABL_KO_BAR"], BWD),
+    "ko_all": (["CUSTMA_ABL_BWD_NOMEM", "CUSTMA_ABL_KO_BAR", "CUSTMA_ABL_KO_RED", "CUSTMA_ABL_KO_SLIDE"], BWD),
     "bdp2ab1": (["CUSTMA_BWD_DEPTH=2", "CUSTMA_BWD_ABUF=1", "CUSTMA_BWD_FBC=6"], BWD),
 }
 for n in (sys.argv[1:] or VARIANTS):
