@@ -644,7 +644,8 @@ __global__ __launch_bounds__(256) void k_bwd_cover(Geo g, int64_t dlo, int nChun
 
 // Sum the partial slots per pixel; out (fp64, [2 sides][4][H][W]): T1, Am|Ac, B|Bp, m'*B.
 template <typename T>
-__global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* acc) {
+__global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* acc, const float* remT,
+                                                    const double* remT1) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t plane = g.H * g.W;
     if (p >= plane) return;
@@ -668,6 +669,16 @@ __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* ac
             }
             if (i < n) v0 += (double)base[(size_t)sl[i] * plane];
             s[q] = v0 + v1;
+        }
+        if (remT) {  // the remainder diagonal's terms (k_bwd_rem_*)
+            const int64_t nyw = (a.yhi - a.ylo) * g.W, nv = g.HV() * g.WO, yy = y - a.ylo, D = g.D;
+            const int64_t w = side == 0 ? x : x - D;  // the voxel column of this pixel on diagonal D
+            if (side == 0 || x >= D - g.r) s[0] += remT1[side * nyw + yy * g.W + x];
+            if (y >= g.h_lo && y < g.h_hi && w >= 0 && w < g.WO) {
+                const int64_t t = (y - g.h_lo) * g.WO + w;
+                s[1] += (double)remT[(2 * side) * nv + t];
+                s[2] += (double)remT[(2 * side + 1) * nv + t];
+            }
         }
     }
     const Stats& st = side == 0 ? a.sc : a.sp;
@@ -799,11 +810,13 @@ __global__ __launch_bounds__(256) void k_bwd_prep(Geo g, const T* __restrict__ c
 // Its voxels (h, w, D) are the last element of every 1028-byte volume row; one strided pass
 // reads them (L2-line granular, ~1/32 of their lines is used, but they are 1/(D+1) of the
 // volume) instead of a fifth chunk of full sweeps with 1 live lane in 64.  Same arithmetic
-// as k_bwd_coop (fp32 A and V, shifted images), added into the gathered sums (fp64):
-//   camera (h, w):  Am += A mp'(h, w+D),  B += V Y(h, w+D),  m'B += V Y mc'(h, w)
-//   projector (h, o = w+D):  Ac += A mc'(h, w),  Bp += V X(h, w),  m'Bp += V X mp'(h, o)
-//   T1c(y, x) += p'(y, x+D) BoxA_D(y, x),  T1p(y, x+D) += c'(y, x) BoxA_D(y, x)
-__global__ __launch_bounds__(256) void k_bwd_rem_voxel(Geo g, BwdArgs a, double* acc, float* remA) {
+// as k_bwd_coop (fp32 A and V, shifted images).  Its terms go to compact arrays that
+// k_bwd_gather adds to the chunks' partial sums (so the three kernels depend on nothing but
+// k_bwd_prep and run beside k_bwd_coop on a second stream):
+//   remT[0..3][h][w] = A mp'(h, w+D), V Y(h, w+D), A mc'(h, w), V X(h, w)   (camera Am, B; projector Ac, Bp
+//   at o = w + D; gather's m' B products then include them)
+//   remT1[0][y][x] = p'(y, x+D) BoxA_D(y, x),  remT1[1][y][x+D] = c'(y, x) BoxA_D(y, x)   (T1c, T1p)
+__global__ __launch_bounds__(256) void k_bwd_rem_voxel(Geo g, BwdArgs a, float* remT, float* remA) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= g.HV() * g.WO) return;
     const int64_t hv = t / g.WO, w = t % g.WO, h = g.h_lo + hv, D = g.D;
@@ -814,15 +827,12 @@ __global__ __launch_bounds__(256) void k_bwd_rem_voxel(Geo g, BwdArgs a, double*
     const float A = a.grad[e] * rS;
     const float V = A * a.vol[e] * rS;
     remA[t] = A;
-    double* c = acc;
-    double* q = acc + 4 * plane;
-    const double vy = (double)(V * Y), vx = (double)(V * X);
-    c[plane + pc] += (double)(A * a.mpp[po]);
-    c[2 * plane + pc] += vy;
-    c[3 * plane + pc] += vy * (double)a.mcc[pc];
-    q[plane + po] += (double)(A * a.mcc[pc]);
-    q[2 * plane + po] += vx;
-    q[3 * plane + po] += vx * (double)a.mpp[po];
+    const int64_t n = g.HV() * g.WO;
+    remT[t] = A * a.mpp[po];
+    remT[n + t] = V * Y;
+    remT[2 * n + t] = A * a.mcc[pc];
+    remT[3 * n + t] = V * X;
+    (void)plane;
 }
 // vertical box of A_D: VA[y - ylo][w] = sum over volume rows h in [y - r, y + r]
 __global__ __launch_bounds__(256) void k_bwd_rem_vbox(Geo g, BwdArgs a, const float* remA, double* remV) {
@@ -837,7 +847,7 @@ __global__ __launch_bounds__(256) void k_bwd_rem_vbox(Geo g, BwdArgs a, const fl
     remV[t] = v;
 }
 // horizontal box and the T1 terms, camera column x in [-r, W) (x < 0: zero padding, c' = -cbar)
-__global__ __launch_bounds__(256) void k_bwd_rem_t1(Geo g, BwdArgs a, const double* remV, double* acc) {
+__global__ __launch_bounds__(256) void k_bwd_rem_t1(Geo g, BwdArgs a, const double* remV, double* remT1) {
     const int64_t nx = g.W + g.r;
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= (a.yhi - a.ylo) * nx) return;
@@ -847,15 +857,15 @@ __global__ __launch_bounds__(256) void k_bwd_rem_t1(Geo g, BwdArgs a, const doub
     w1 = w1 < g.WO - 1 ? w1 : g.WO - 1;
     double box = 0.0;
     for (int64_t w = w0; w <= w1; ++w) box += remV[yy * g.WO + w];
-    const int64_t plane = g.H * g.W;
+    const int64_t nyw = (a.yhi - a.ylo) * g.W;
     const float cb = a.shift[0], pb = a.shift[1];
     if (x >= 0) {  // camera pixel (y, x): p'(y, x + D), zero padded past the right edge
         const float pv = x + D < g.W ? a.pp[y * g.W + x + D] : 0.f;
-        acc[y * g.W + x] += (double)(pv - pb) * box;
+        remT1[yy * g.W + x] = (double)(pv - pb) * box;
     }
-    if (x + D >= 0 && x + D < g.W) {  // projector pixel (y, x + D)
+    if (x + D >= 0 && x + D < g.W) {  // projector pixel (y, x + D); o < D - r gets no term (gather checks)
         const float cv = x >= 0 ? a.cc[y * g.W + x] : 0.f;
-        acc[4 * plane + y * g.W + x + D] += (double)(cv - cb) * box;
+        remT1[nyw + yy * g.W + x + D] = (double)(cv - cb) * box;
     }
 }
 
@@ -939,10 +949,36 @@ BwdPlan plan_bwd(const Geo& g) {
     p.prep_bytes = 6 * plane * sizeof(float);
     p.misc_bytes = 2 * kSumBlocks * sizeof(double) + 256;
     // A of diagonal D [HV][WO] (fp32) and its vertical box [yhi - ylo][WO] (fp64)
-    p.rem_bytes = p.rem ? a256((size_t)g.HV() * g.WO * 4) + (size_t)(p.yhi - p.ylo) * g.WO * 8 : 0;
+    // remA [HV][WO] f32, its vertical box [yhi - ylo][WO] f64, remT [4][HV][WO] f32, remT1 [2][yhi - ylo][W] f64
+    p.rem_bytes = p.rem ? a256((size_t)g.HV() * g.WO * 4) + a256((size_t)(p.yhi - p.ylo) * g.WO * 8) +
+                              a256((size_t)4 * g.HV() * g.WO * 4) + (size_t)2 * (p.yhi - p.ylo) * g.W * 8
+                        : 0;
     return p;
 }
 
+
+// A second stream (and its fork / join events) per host thread and device, for work that may
+// overlap the sweep; created on first use, kept for the thread's life.
+struct SideStream {
+    hipStream_t st = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+hipError_t side_stream(SideStream** out) {
+    constexpr int kMaxDev = 64;
+    thread_local SideStream tab[kMaxDev];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    SideStream& ss = tab[dev];
+    if (!ss.st) {
+        if ((e = hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    *out = &ss;
+    return hipSuccess;
+}
 
 template <typename T>
 hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp,
@@ -976,6 +1012,36 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     a.dlo = p.dlo; a.ylo = p.ylo; a.yhi = p.yhi;
     a.order = g.layout == CUSTMA_LAYOUT_WINDOW ? 2 : 1;
     if (const char* eo = getenv("CUSTMA_BWD_ORDER")) a.order = atoi(eo);  // benchmarking only
+    // The remainder diagonal's kernels need only k_bwd_prep: they run on a second stream beside
+    // k_bwd_coop (their strided, latency-bound reads overlap the sweep) and k_bwd_gather waits
+    // for both.  CUSTMA_BWD_REM_SIDE=0 keeps them on the caller's stream (benchmarking only).
+    float* remT = nullptr;
+    double* remT1 = nullptr;
+    SideStream* side = nullptr;
+    if (p.rem) {
+        char* rw = (char*)bsum + a256(p.misc_bytes);  // the plan's rem_bytes follow misc_bytes
+        const size_t nA = a256((size_t)g.HV() * g.WO * 4), nV = a256((size_t)(p.yhi - p.ylo) * g.WO * 8);
+        float* remA = (float*)rw;
+        double* remV = (double*)(rw + nA);
+        remT = (float*)(rw + nA + nV);
+        remT1 = (double*)(rw + nA + nV + a256((size_t)4 * g.HV() * g.WO * 4));
+        hipStream_t rs = s;
+        const char* es = getenv("CUSTMA_BWD_REM_SIDE");
+        if (!(es && atoi(es) == 0)) {
+            if ((e = side_stream(&side)) != hipSuccess) return e;
+            if ((e = hipEventRecord(side->fork, s)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(side->st, side->fork, 0)) != hipSuccess) return e;
+            rs = side->st;
+        }
+        hipLaunchKernelGGL(k_bwd_rem_voxel, dim3((unsigned)cdiv(g.HV() * g.WO, 256)), dim3(256), 0, rs, g, a, remT,
+                           remA);
+        hipLaunchKernelGGL(k_bwd_rem_vbox, dim3((unsigned)cdiv((p.yhi - p.ylo) * g.WO, 256)), dim3(256), 0, rs, g, a,
+                           remA, remV);
+        hipLaunchKernelGGL(k_bwd_rem_t1, dim3((unsigned)cdiv((p.yhi - p.ylo) * (g.W + g.r), 256)), dim3(256), 0, rs,
+                           g, a, remV, remT1);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (side && (e = hipEventRecord(side->join, side->st)) != hipSuccess) return e;
+    }
     const int64_t units = (int64_t)p.nChunk * p.nsegMax * p.nRG;
     const unsigned blocks = (unsigned)(8 * (int64_t)p.nChunk * p.nsegMax * cdiv(p.nRG, 8));
     if (units > 0) {
@@ -990,18 +1056,8 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
         prof_end(PROF_BWD, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc);
-    if (p.rem) {
-        char* rw = (char*)bsum + a256(p.misc_bytes);  // the plan's rem_bytes follow misc_bytes
-        float* remA = (float*)rw;
-        double* remV = (double*)(rw + a256((size_t)g.HV() * g.WO * 4));
-        hipLaunchKernelGGL(k_bwd_rem_voxel, dim3((unsigned)cdiv(g.HV() * g.WO, 256)), dim3(256), 0, s, g, a, acc,
-                           remA);
-        hipLaunchKernelGGL(k_bwd_rem_vbox, dim3((unsigned)cdiv((p.yhi - p.ylo) * g.WO, 256)), dim3(256), 0, s, g, a,
-                           remA, remV);
-        hipLaunchKernelGGL(k_bwd_rem_t1, dim3((unsigned)cdiv((p.yhi - p.ylo) * (g.W + g.r), 256)), dim3(256), 0, s,
-                           g, a, remV, acc);
-    }
+    if (side && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc, remT, remT1);
     const int L = 16 + 2 * g.r;
     hipLaunchKernelGGL(k_bwd_combine2<T>, dim3((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2), dim3(256),
                        sizeof(double) * 3 * (L * L + L * 16), s, g, cam, proj, shift, acc, dcam, dproj);
