@@ -66,6 +66,13 @@ def _check_hazards(unit, extra, libdir):
     if r.returncode != 0:
         os.remove(_obj(unit, libdir))
         raise RuntimeError(f"wait-state hazards in {name} ({src}):\n{r.stdout}")
+    # The hand-pipelined kernels must not spill VGPRs to scratch: the compiler takes an asm
+    # load's destination as written when the asm issues, so a spill could store it in flight.
+    with open(listing) as f:
+        scratch = [ln.strip() for ln in f if ln.startswith("; ScratchSize:") and ln.split(":")[1].strip() != "0"]
+    if scratch:
+        os.remove(_obj(unit, libdir))
+        raise RuntimeError(f"scratch use in {name} ({src}): {scratch[:4]}")
     os.remove(listing)
 
 

@@ -124,15 +124,12 @@ struct DispPartial {
 // weights are taken relative to the running best (rescaled when it grows), so they never
 // overflow; invalid entries (-FLT_MAX) carry no weight.
 __device__ __forceinline__ void soft_add(float v, float idx, float best_before, float kb, float& s0, float& s1) {
-    if (v > best_before) {
-        const float sc = __builtin_amdgcn_exp2f(kb * (best_before - v));
-        s0 = s0 * sc + 1.f;
-        s1 = s1 * sc + idx;
-    } else {
-        const float wgt = __builtin_amdgcn_exp2f(kb * (v - best_before));
-        s0 += wgt;
-        s1 += wgt * idx;
-    }
+    // branch-free, one exp2: a new best rescales the sums by exp2(kb (best_before - v)) and adds
+    // weight 1, otherwise the element adds exp2(kb (v - best_before))
+    const bool gt = v > best_before;
+    const float e = __builtin_amdgcn_exp2f(kb * (gt ? best_before - v : v - best_before));
+    s0 = gt ? s0 * e + 1.f : s0 + e;
+    s1 = gt ? s1 * e + idx : s1 + e * idx;
 }
 // merge another accumulator (bo, o0, o1) into (b, s0, s1); both relative to their own best
 __device__ __forceinline__ void soft_merge(float b, float bo, float o0, float o1, float kb, float& s0, float& s1) {

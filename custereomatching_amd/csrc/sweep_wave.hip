@@ -367,11 +367,16 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
 #pragma unroll
                     for (int ps = 0; ps < AMX; ++ps) {
                         const int m = (ps * nw + wv) * 4 + (l >> 4);  // tile row of this 16-lane group
+                        // one scan chain per lane, then the 16 lanes of the row combined by DPP row
+                        // rotations (8, 4, 2, 1: every lane meets each other lane's part once)
                         float b = -FLT_MAX, sec = -FLT_MAX, q0 = 0.f, q1 = 0.f;
                         int bi = INT_MAX;
                         // increasing s per lane: the first index wins among equal values
                         const int mr = m < TW ? m : 0;
-#pragma unroll
+                        // partly unrolled: fully unrolled, the compiler hoists all 17 LDS reads (and
+                        // the soft sums' exp2 operands) and the kernel needs 168-206 VGPRs; 6 (3 with
+                        // the soft sums) keeps every variant at 149-155 VGPRs, 3 waves per SIMD
+#pragma unroll SOFT ? 3 : 6
                         for (int i = 0; i < (64 * kTileMaxChunks + 1 + 15) / 16; ++i) {
                             const int s2 = sub + 16 * i;
                             if (s2 < (int)DO) {
@@ -383,17 +388,18 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                                 b = gt ? v : b;
                             }
                         }
-#pragma unroll
-                        for (int off = 8; off > 0; off >>= 1) {
-                            const float ob = __shfl_xor(b, off), os = __shfl_xor(sec, off);
-                            const int oi = __shfl_xor(bi, off);
-                            if (soft) {
-                                const float o0 = __shfl_xor(q0, off), o1 = __shfl_xor(q1, off);
-                                soft_merge(b, ob, o0, o1, kb, q0, q1);
-                            }
+                        Unroll<0, 4>::run([&](auto lc) {
+                            constexpr int ctrl = 0x120 + (8 >> decltype(lc)::value);  // row_ror:8, 4, 2, 1
+                            auto rot = [&](float x) {
+                                return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                    0, __builtin_bit_cast(int, x), ctrl, 0xf, 0xf, false));
+                            };
+                            const float ob = rot(b), os = rot(sec);
+                            const int oi = __builtin_amdgcn_update_dpp(0, bi, ctrl, 0xf, 0xf, false);
+                            if (soft) soft_merge(b, ob, rot(q0), rot(q1), kb, q0, q1);
                             if (ob > b || (ob == b && oi < bi)) { sec = fmaxf(os, b); b = ob; bi = oi; }
                             else sec = fmaxf(sec, ob);
-                        }
+                        });
                         const uint32_t vo = (sub == 0 && m < TW) ? (uint32_t)(m * 4) : OOB;
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, b), rB, vo, 0u, 0);
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, sec), rS, vo, 0u, 0);

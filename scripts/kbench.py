@@ -54,6 +54,12 @@ def run(name, ops, reps):
             nre = et.record(lambda: cm.stereo_disparity(cam, proj, D, k, lay, return_rechecked=True))
         res["disp_ms"] = round(et.mean_ms(), 4)
         res["disp_rechecked"] = int(nre[2].item())
+    if "soft" in ops:
+        cm.stereo_disparity_soft(cam, proj, D, k, lay)
+        et = EventTimer()
+        for _ in range(reps):
+            et.record(lambda: cm.stereo_disparity_soft(cam, proj, D, k, lay))
+        res["soft_ms"] = round(et.mean_ms(), 4)
     torch.cuda.empty_cache()
     return res
 
