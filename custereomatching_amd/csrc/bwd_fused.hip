@@ -642,6 +642,39 @@ __global__ __launch_bounds__(256) void k_bwd_cover(Geo g, int64_t dlo, int nChun
     }
 }
 
+// Sum of the partial slots of type 3 side + q at pixel p = (y, x) (fp64, even / odd slots in two
+// accumulators, in the cover list's order), plus the remainder diagonal's term of that type
+// (k_bwd_rem_*).  The caller checks y in [ylo, yhi).
+__device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, const float* remT, const double* remT1,
+                                             int side, int q, int64_t y, int64_t x, int64_t p) {
+    const int64_t plane = g.H * g.W;
+    const unsigned short* list = (const unsigned short*)(a.cover + 3 * g.W);
+    const int t = 3 * side + q;
+    const int cls = side == 0 ? 0 : (q == 0 ? 1 : 2);
+    const int n = a.cover[cls * g.W + x];
+    const unsigned short* sl = list + ((size_t)cls * g.W + x) * a.S;
+    const float* base = a.part + (size_t)t * a.S * plane + p;
+    double v0 = 0.0, v1 = 0.0;
+    int i = 0;
+    for (; i + 1 < n; i += 2) {
+        v0 += (double)base[(size_t)sl[i] * plane];
+        v1 += (double)base[(size_t)sl[i + 1] * plane];
+    }
+    if (i < n) v0 += (double)base[(size_t)sl[i] * plane];
+    double s = v0 + v1;
+    if (remT) {  // the remainder diagonal's terms (k_bwd_rem_*)
+        const int64_t nyw = (a.yhi - a.ylo) * g.W, nv = g.HV() * g.WO, yy = y - a.ylo, D = g.D;
+        if (q == 0) {
+            if (side == 0 || x >= D - g.r) s += remT1[side * nyw + yy * g.W + x];
+        } else {
+            const int64_t w = side == 0 ? x : x - D;  // the voxel column of this pixel on diagonal D
+            if (y >= g.h_lo && y < g.h_hi && w >= 0 && w < g.WO)
+                s += (double)remT[(2 * side + q - 1) * nv + (y - g.h_lo) * g.WO + w];
+        }
+    }
+    return s;
+}
+
 // Sum the partial slots per pixel; out (fp64, [2 sides][4][H][W]): T1, Am|Ac, B|Bp, m'*B.
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* acc, const float* remT,
@@ -651,35 +684,10 @@ __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* ac
     if (p >= plane) return;
     const int64_t y = p / g.W, x = p % g.W;
     const int side = blockIdx.y;
-    const unsigned short* list = (const unsigned short*)(a.cover + 3 * g.W);
     double s[3] = {0.0, 0.0, 0.0};
     if (y >= a.ylo && y < a.yhi) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const int t = 3 * side + q;
-            const int cls = side == 0 ? 0 : (q == 0 ? 1 : 2);
-            const int n = a.cover[cls * g.W + x];
-            const unsigned short* sl = list + ((size_t)cls * g.W + x) * a.S;
-            const float* base = a.part + (size_t)t * a.S * plane + p;
-            double v0 = 0.0, v1 = 0.0;
-            int i = 0;
-            for (; i + 1 < n; i += 2) {
-                v0 += (double)base[(size_t)sl[i] * plane];
-                v1 += (double)base[(size_t)sl[i + 1] * plane];
-            }
-            if (i < n) v0 += (double)base[(size_t)sl[i] * plane];
-            s[q] = v0 + v1;
-        }
-        if (remT) {  // the remainder diagonal's terms (k_bwd_rem_*)
-            const int64_t nyw = (a.yhi - a.ylo) * g.W, nv = g.HV() * g.WO, yy = y - a.ylo, D = g.D;
-            const int64_t w = side == 0 ? x : x - D;  // the voxel column of this pixel on diagonal D
-            if (side == 0 || x >= D - g.r) s[0] += remT1[side * nyw + yy * g.W + x];
-            if (y >= g.h_lo && y < g.h_hi && w >= 0 && w < g.WO) {
-                const int64_t t = (y - g.h_lo) * g.WO + w;
-                s[1] += (double)remT[(2 * side) * nv + t];
-                s[2] += (double)remT[(2 * side + 1) * nv + t];
-            }
-        }
+        for (int q = 0; q < 3; ++q) s[q] = gather_sum(g, a, remT, remT1, side, q, y, x, p);
     }
     const Stats& st = side == 0 ? a.sc : a.sp;
     const double sh = side == 0 ? (double)a.shift[0] : (double)a.shift[1];
@@ -1057,10 +1065,13 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (side && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc, remT, remT1);
+    // (gather and combine fused into one tiled pass -- the slot sums recomputed for each tile's r
+    // halo -- measured slower: C5 backward op 29.5 -> 31.1 ms, C2 full 3.82 -> 3.95 ms)
     const int L = 16 + 2 * g.r;
-    hipLaunchKernelGGL(k_bwd_combine2<T>, dim3((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2), dim3(256),
-                       sizeof(double) * 3 * (L * L + L * 16), s, g, cam, proj, shift, acc, dcam, dproj);
+    const size_t lds = sizeof(double) * 3 * (L * L + L * 16);
+    const dim3 tiles((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2);
+    hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc, remT, remT1);
+    hipLaunchKernelGGL(k_bwd_combine2<T>, tiles, dim3(256), lds, s, g, cam, proj, shift, acc, dcam, dproj);
     return hipGetLastError();
 }
 
