@@ -84,9 +84,9 @@ void carve_stats(const Geo& g, void* ws, Stats* sc, Stats* sp) {
 }
 
 int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, void* ws, Stats* sc, Stats* sp,
-              hipStream_t s) {
+              hipStream_t s, bool box_only = false) {
     carve_stats(g, ws, sc, sp);
-    return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s), "stats");
+    return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s, box_only), "stats");
 }
 
 int check_dtype(int32_t dtype) {
@@ -259,7 +259,9 @@ int custma_backward_band(const float* grad, const float* cost_volume, const void
     const size_t need = stats_bytes(g) + align256(bwd_bytes(g)) + (cost_volume ? 0 : align256(volume_bytes(g)));
     if (workspace_bytes < need) return fail(CUSTMA_E_WORKSPACE, "workspace too small (%zu < %zu)", workspace_bytes, need);
     Stats sc, sp;
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
+    // with the forward's volume given, the backward reads only box and sqt (bwd_fused.hip,
+    // bwd_generic.hip): the two k^2-long fp32 chains of mean / sq are skipped
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, cost_volume != nullptr))) return rc;
     char* ws2 = (char*)workspace + stats_bytes(g);
     if (!cost_volume) {  // recompute the forward into the workspace
         float* vol = (float*)(ws2 + align256(bwd_bytes(g)));

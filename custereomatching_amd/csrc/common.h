@@ -299,7 +299,9 @@ inline hipError_t allow_lds(F* kernel, size_t bytes) {
 namespace custma {
 hipError_t launch_u8_to_unit(const uint8_t* src, int64_t npix, int C, int ch, int out_dtype, void* out,
                              hipStream_t s);
-hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s);
+// box_only: only box and sqt (what the backward reads); mean and sq are left unwritten
+hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
+                        bool box_only = false);
 hipError_t launch_fwd_exact(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             float* out, hipStream_t s);
 hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,

@@ -20,10 +20,13 @@ namespace custma {
 
 namespace {
 constexpr int TX = 16, TY = 64, PR = 4;  // 16 x 64 pixels per 256-thread workgroup, 4 rows per thread
+static_assert(PR % 2 == 0, "pixel pairs");
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // KT > 0: the window size as a compile-time constant (the sweep's instantiations), so the
 // k^2 tap loops unroll and the per-pixel row masks fold away; KT = 0: runtime k.
-template <typename T, int KT>
+// BOX_ONLY: box and sqt only (the backward's statistics; mean and sq are not written).
+template <typename T, int KT, bool BOX_ONLY = false>
 __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const T* __restrict__ img1, Geo g,
                                                Stats st0, Stats st1) {
     // blockIdx.z: 0 = camera, 1 = projector (one launch for both images)
@@ -55,6 +58,27 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
     }
     __syncthreads();
     const int lx = threadIdx.x % TX, q = threadIdx.x / TX;  // rows PR q .. PR q + PR-1
+    if constexpr (BOX_ONLY) {
+        const int64_t x = x0 + lx;
+        if (x >= g.W) return;
+#pragma unroll
+        for (int p = 0; p < PR; ++p) {
+            const int ly = PR * q + p;
+            const int64_t y = y0 + ly;
+            if (y >= g.H) break;
+            double b = 0.0, b2 = 0.0;
+#pragma unroll
+            for (int i = 0; i < k; ++i) {
+                b += rs[(ly + i) * TX + lx];
+                b2 += rs2[(ly + i) * TX + lx];
+            }
+            const int64_t o = y * g.W + x;
+            st.box[o] = b;
+            const double c2 = b2 - b * b / (double)(k * k);
+            st.sqt[o] = (float)(c2 > 0.0 ? c2 : 0.0);
+        }
+        return;
+    }
     // Each tile value is read once per pass and fed to the PR pixels whose patch holds it;
     // per pixel the taps still arrive in the reference's (i, j) row-major order.
     const float* t = tile + (PR * q) * LX + lx;
@@ -70,12 +94,23 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
         if constexpr (KT > 0) {
 #pragma unroll
             for (int j = 0; j < KT; ++j) v[j] = t[i2 * LX + j];
+            if (i2 >= PR - 1 && i2 < k) {  // the row is in all PR patches: pixel pairs in packed fp32 adds
 #pragma unroll
-            for (int p = 0; p < PR; ++p)
-                if (i2 - p >= 0 && i2 - p < k) {
+                for (int pp = 0; pp < PR / 2; ++pp) {
+                    f32x2 a = {m[2 * pp], m[2 * pp + 1]};
 #pragma unroll
-                    for (int j = 0; j < KT; ++j) m[p] = m[p] + v[j];
+                    for (int j = 0; j < KT; ++j) a = a + f32x2{v[j], v[j]};
+                    m[2 * pp] = a.x;
+                    m[2 * pp + 1] = a.y;
                 }
+            } else {
+#pragma unroll
+                for (int p = 0; p < PR; ++p)
+                    if (i2 - p >= 0 && i2 - p < k) {
+#pragma unroll
+                        for (int j = 0; j < KT; ++j) m[p] = m[p] + v[j];
+                    }
+            }
         } else {
             for (int j = 0; j < k; ++j) {
                 const float u = t[i2 * LX + j];
@@ -93,15 +128,30 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
         if constexpr (KT > 0) {
 #pragma unroll
             for (int j = 0; j < KT; ++j) v[j] = t[i2 * LX + j];
+            if (i2 >= PR - 1 && i2 < k) {  // packed: v_pk_add_f32 / v_pk_fma_f32, the same IEEE ops per lane half
 #pragma unroll
-            for (int p = 0; p < PR; ++p)
-                if (i2 - p >= 0 && i2 - p < k) {
+                for (int pp = 0; pp < PR / 2; ++pp) {
+                    const f32x2 mm = {m[2 * pp], m[2 * pp + 1]};
+                    f32x2 a = {sq[2 * pp], sq[2 * pp + 1]};
 #pragma unroll
                     for (int j = 0; j < KT; ++j) {
-                        const float c = v[j] - m[p];
-                        sq[p] = __builtin_fmaf(c, c, sq[p]);
+                        const f32x2 c = f32x2{v[j], v[j]} - mm;
+                        a = __builtin_elementwise_fma(c, c, a);
                     }
+                    sq[2 * pp] = a.x;
+                    sq[2 * pp + 1] = a.y;
                 }
+            } else {
+#pragma unroll
+                for (int p = 0; p < PR; ++p)
+                    if (i2 - p >= 0 && i2 - p < k) {
+#pragma unroll
+                        for (int j = 0; j < KT; ++j) {
+                            const float c = v[j] - m[p];
+                            sq[p] = __builtin_fmaf(c, c, sq[p]);
+                        }
+                    }
+            }
         } else {
             for (int j = 0; j < k; ++j) {
                 const float u = t[i2 * LX + j];
@@ -137,22 +187,26 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
 }
 }  // namespace
 
-hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s) {
+hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
+                        bool box_only) {
     const dim3 grid((unsigned)cdiv(g.W, TX), (unsigned)cdiv(g.H, TY), 2);
     const int LX = TX + 2 * g.r, LY = TY + 2 * g.r;
     const size_t lds = sizeof(double) * 2 * LY * TX + sizeof(float) * LY * LX;
     hipError_t err = hipSuccess;
     auto go = [&](auto kc) {
         constexpr int KT = decltype(kc)::value;
-        if (dtype == CUSTMA_F16) {
-            if ((err = allow_lds(k_stats<__half, KT>, lds)) != hipSuccess) return;
-            hipLaunchKernelGGL((k_stats<__half, KT>), grid, dim3(256), lds, s, (const __half*)cam, (const __half*)proj,
-                               g, sc, sp);
-        } else {
-            if ((err = allow_lds(k_stats<float, KT>, lds)) != hipSuccess) return;
-            hipLaunchKernelGGL((k_stats<float, KT>), grid, dim3(256), lds, s, (const float*)cam, (const float*)proj, g,
-                               sc, sp);
-        }
+        auto launch = [&](auto* cast, auto bc) {
+            using T = std::remove_const_t<std::remove_pointer_t<decltype(cast)>>;
+            constexpr bool BO = decltype(bc)::value;
+            if ((err = allow_lds(k_stats<T, KT, BO>, lds)) != hipSuccess) return;
+            hipLaunchKernelGGL((k_stats<T, KT, BO>), grid, dim3(256), lds, s, (const T*)cam, (const T*)proj, g, sc, sp);
+        };
+        auto by_mode = [&](auto* cast) {
+            if (box_only) launch(cast, std::true_type{});
+            else launch(cast, std::false_type{});
+        };
+        if (dtype == CUSTMA_F16) by_mode((const __half*)nullptr);
+        else by_mode((const float*)nullptr);
     };
     switch (g.k) {
 #define CUSTMA_K(KK) \
