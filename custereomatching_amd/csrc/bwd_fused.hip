@@ -679,11 +679,12 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* acc, const float* remT,
                                                     const double* remT1) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // blockIdx.y = the image row, x = the column, z = the side (no 64-bit division per thread)
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     const int64_t plane = g.H * g.W;
-    if (p >= plane) return;
-    const int64_t y = p / g.W, x = p % g.W;
-    const int side = blockIdx.y;
+    if (x >= g.W) return;
+    const int64_t p = y * g.W + x;
+    const int side = blockIdx.z;
     double s[3] = {0.0, 0.0, 0.0};
     if (y >= a.ylo && y < a.yhi) {
 #pragma unroll
@@ -824,10 +825,11 @@ __global__ __launch_bounds__(256) void k_bwd_prep(Geo g, const T* __restrict__ c
 //   remT[0..3][h][w] = A mp'(h, w+D), V Y(h, w+D), A mc'(h, w), V X(h, w)   (camera Am, B; projector Ac, Bp
 //   at o = w + D; gather's m' B products then include them)
 //   remT1[0][y][x] = p'(y, x+D) BoxA_D(y, x),  remT1[1][y][x+D] = c'(y, x) BoxA_D(y, x)   (T1c, T1p)
+// (2-D grids: blockIdx.y = the row, x = the column -- no 64-bit division per thread)
 __global__ __launch_bounds__(256) void k_bwd_rem_voxel(Geo g, BwdArgs a, float* remT, float* remA) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= g.HV() * g.WO) return;
-    const int64_t hv = t / g.WO, w = t % g.WO, h = g.h_lo + hv, D = g.D;
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x, hv = blockIdx.y;
+    if (w >= g.WO) return;
+    const int64_t t = hv * g.WO + w, h = g.h_lo + hv, D = g.D;
     const int64_t plane = g.H * g.W, pc = h * g.W + w, po = pc + D;
     const int64_t e = t * g.DO + D;
     const float X = a.Xc[pc], Y = a.Yp[po];
@@ -844,9 +846,9 @@ __global__ __launch_bounds__(256) void k_bwd_rem_voxel(Geo g, BwdArgs a, float* 
 }
 // vertical box of A_D: VA[y - ylo][w] = sum over volume rows h in [y - r, y + r]
 __global__ __launch_bounds__(256) void k_bwd_rem_vbox(Geo g, BwdArgs a, const float* remA, double* remV) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= (a.yhi - a.ylo) * g.WO) return;
-    const int64_t y = a.ylo + t / g.WO, w = t % g.WO;
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w >= g.WO) return;
+    const int64_t t = (int64_t)blockIdx.y * g.WO + w, y = a.ylo + blockIdx.y;
     int64_t h0 = y - g.r, h1 = y + g.r;
     h0 = h0 > g.h_lo ? h0 : g.h_lo;
     h1 = h1 < g.h_hi - 1 ? h1 : g.h_hi - 1;
@@ -856,10 +858,9 @@ __global__ __launch_bounds__(256) void k_bwd_rem_vbox(Geo g, BwdArgs a, const fl
 }
 // horizontal box and the T1 terms, camera column x in [-r, W) (x < 0: zero padding, c' = -cbar)
 __global__ __launch_bounds__(256) void k_bwd_rem_t1(Geo g, BwdArgs a, const double* remV, double* remT1) {
-    const int64_t nx = g.W + g.r;
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= (a.yhi - a.ylo) * nx) return;
-    const int64_t yy = t / nx, x = t % nx - g.r, y = a.ylo + yy, D = g.D;
+    const int64_t xi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (xi >= g.W + g.r) return;
+    const int64_t yy = blockIdx.y, x = xi - g.r, y = a.ylo + yy, D = g.D;
     int64_t w0 = x - g.r, w1 = x + g.r;
     w0 = w0 > 0 ? w0 : 0;
     w1 = w1 < g.WO - 1 ? w1 : g.WO - 1;
@@ -1041,12 +1042,12 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
             if ((e = hipStreamWaitEvent(side->st, side->fork, 0)) != hipSuccess) return e;
             rs = side->st;
         }
-        hipLaunchKernelGGL(k_bwd_rem_voxel, dim3((unsigned)cdiv(g.HV() * g.WO, 256)), dim3(256), 0, rs, g, a, remT,
-                           remA);
-        hipLaunchKernelGGL(k_bwd_rem_vbox, dim3((unsigned)cdiv((p.yhi - p.ylo) * g.WO, 256)), dim3(256), 0, rs, g, a,
-                           remA, remV);
-        hipLaunchKernelGGL(k_bwd_rem_t1, dim3((unsigned)cdiv((p.yhi - p.ylo) * (g.W + g.r), 256)), dim3(256), 0, rs,
-                           g, a, remV, remT1);
+        hipLaunchKernelGGL(k_bwd_rem_voxel, dim3((unsigned)cdiv(g.WO, 256), (unsigned)g.HV()), dim3(256), 0, rs, g, a,
+                           remT, remA);
+        hipLaunchKernelGGL(k_bwd_rem_vbox, dim3((unsigned)cdiv(g.WO, 256), (unsigned)(p.yhi - p.ylo)), dim3(256), 0, rs,
+                           g, a, remA, remV);
+        hipLaunchKernelGGL(k_bwd_rem_t1, dim3((unsigned)cdiv(g.W + g.r, 256), (unsigned)(p.yhi - p.ylo)), dim3(256), 0,
+                           rs, g, a, remV, remT1);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (side && (e = hipEventRecord(side->join, side->st)) != hipSuccess) return e;
     }
@@ -1070,7 +1071,8 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     const int L = 16 + 2 * g.r;
     const size_t lds = sizeof(double) * 3 * (L * L + L * 16);
     const dim3 tiles((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2);
-    hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(n, 256), 2), dim3(256), 0, s, g, a, acc, remT, remT1);
+    hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2), dim3(256), 0, s, g, a, acc,
+                       remT, remT1);
     hipLaunchKernelGGL(k_bwd_combine2<T>, tiles, dim3(256), lds, s, g, cam, proj, shift, acc, dcam, dproj);
     return hipGetLastError();
 }
