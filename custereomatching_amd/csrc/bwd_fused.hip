@@ -981,7 +981,16 @@ hipError_t side_stream(SideStream** out) {
     if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
     SideStream& ss = tab[dev];
     if (!ss.st) {
-        if ((e = hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking)) != hipSuccess) return e;
+        // CUSTMA_BWD_REM_PRIO=1: the side stream at the device's lowest priority, so the sweep's
+        // workgroups are dispatched first and the side kernels fill its tail (benchmarking)
+        int prio = 0;
+        const char* ep = getenv("CUSTMA_BWD_REM_PRIO");
+        if (ep && atoi(ep) == 1) {
+            int least = 0, greatest = 0;
+            if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return e;
+            prio = least;
+        }
+        if ((e = hipStreamCreateWithPriority(&ss.st, hipStreamNonBlocking, prio)) != hipSuccess) return e;
         if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return e;
         if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return e;
     }
