@@ -66,14 +66,20 @@ def _check_hazards(unit, extra, libdir):
     if r.returncode != 0:
         os.remove(_obj(unit, libdir))
         raise RuntimeError(f"wait-state hazards in {name} ({src}):\n{r.stdout}")
-    # The hand-pipelined kernels must not spill VGPRs to scratch: the compiler takes an asm
-    # load's destination as written when the asm issues, so a spill could store it in flight.
     with open(listing) as f:
-        scratch = [ln.strip() for ln in f if ln.startswith("; ScratchSize:") and ln.split(":")[1].strip() != "0"]
+        scratch = scratch_lines(f.read())
     if scratch:
         os.remove(_obj(unit, libdir))
         raise RuntimeError(f"scratch use in {name} ({src}): {scratch[:4]}")
     os.remove(listing)
+
+
+def scratch_lines(listing: str):
+    """The `; ScratchSize: N` lines of a device listing with N != 0.  The hand-pipelined kernels
+    must not spill VGPRs to scratch: the compiler takes an asm load's destination as written when
+    the asm issues, so a spill could store it while the load is still in flight."""
+    return [ln.strip() for ln in listing.splitlines()
+            if ln.startswith("; ScratchSize:") and ln.split(":", 1)[1].strip() != "0"]
 
 
 def _headers():

@@ -79,3 +79,11 @@ def test_shipped_backward_listing_is_clean(tmp_path):
                         "--cuda-device-only", "-S", src, "-o", str(out)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     assert hc.main(["hazard_check.py", str(out)]) == 0
+
+
+def test_build_rejects_scratch_use():
+    from custereomatching_amd.build import scratch_lines
+    ok = "k_a:\n; ScratchSize: 0\n; Occupancy: 3\nk_b:\n; ScratchSize: 0\n"
+    bad = "k_a:\n; ScratchSize: 0\nk_b:\n; ScratchSize: 28\n"
+    assert scratch_lines(ok) == []
+    assert scratch_lines(bad) == ["; ScratchSize: 28"]
