@@ -675,7 +675,8 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
     return s;
 }
 
-// Sum the partial slots per pixel; out (fp64, [2 sides][4][H][W]): T1, Am|Ac, B|Bp, m'*B.
+// Sum the partial slots per pixel; out (fp64, [2 sides][3][H][W]): T1, Am|Ac, B|Bp (k_bwd_combine2
+// forms m' B as it loads its tile -- the same product, one fp64 array less through HBM).
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* acc, const float* remT,
                                                     const double* remT1) {
@@ -690,21 +691,18 @@ __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* ac
 #pragma unroll
         for (int q = 0; q < 3; ++q) s[q] = gather_sum(g, a, remT, remT1, side, q, y, x, p);
     }
-    const Stats& st = side == 0 ? a.sc : a.sp;
-    const double sh = side == 0 ? (double)a.shift[0] : (double)a.shift[1];
-    const double mprime = st.box[p] / (double)(g.k * g.k) - sh;
-    double* o = acc + (size_t)side * 4 * plane;
+    double* o = acc + (size_t)side * 3 * plane;
     o[p] = s[0];
     o[plane + p] = s[1];
     o[2 * plane + p] = s[2];
-    o[3 * plane + p] = s[2] * mprime;
 }
 
 // grad(y,x) = T1 - Box[A] - img'(y,x) Box[B] + Box[m' B]   (one side per blockIdx.z)
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict__ cam, const T* __restrict__ proj,
                                                       const float* __restrict__ shift, const double* __restrict__ acc,
-                                                      float* __restrict__ dcam, float* __restrict__ dproj) {
+                                                      Stats sc, Stats sp, float* __restrict__ dcam,
+                                                      float* __restrict__ dproj) {
     constexpr int TS = 16;
     extern __shared__ __attribute__((aligned(16))) double tl[];
     const int side = blockIdx.z;
@@ -712,10 +710,11 @@ __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict
     if (!out) return;
     const T* img = side == 0 ? cam : proj;
     const int64_t plane = g.H * g.W;
-    const double* T1 = acc + (size_t)side * 4 * plane;
+    const double* T1 = acc + (size_t)side * 3 * plane;
     const double* Aa = T1 + plane;
     const double* Bb = Aa + plane;
-    const double* MB = Bb + plane;
+    const double* box = side == 0 ? sc.box : sp.box;
+    const double sh = (double)shift[side], rk2 = (double)(g.k * g.k);
     const int r = g.r, L = TS + 2 * r;
     double* tA = tl;
     double* tB = tA + L * L;
@@ -725,9 +724,10 @@ __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict
         const int64_t y = y0 + e / L - r, x = x0 + e % L - r;
         const bool ok = y >= 0 && y < g.H && x >= 0 && x < g.W;
         const int64_t q = y * g.W + x;
+        const double b = ok ? Bb[q] : 0.0;
         tA[e] = ok ? Aa[q] : 0.0;
-        tB[e] = ok ? Bb[q] : 0.0;
-        tM[e] = ok ? MB[q] : 0.0;
+        tB[e] = b;
+        tM[e] = ok ? b * (box[q] / rk2 - sh) : 0.0;  // m' B (as k_bwd_gather formed it before)
     }
     __syncthreads();
     // separable box (fixed order, deterministic): k-tap row sums of the L x TS columns the
@@ -953,7 +953,7 @@ BwdPlan plan_bwd(const Geo& g) {
     p.nRG = (int)cdiv(p.yhi - p.ylo, TRB);
     const size_t plane = (size_t)g.H * g.W;
     p.part_bytes = (size_t)NTYPE * p.S * plane * sizeof(float);
-    p.acc_bytes = 8 * plane * sizeof(double);
+    p.acc_bytes = 6 * plane * sizeof(double);
     p.cover_bytes = 3 * (size_t)g.W * sizeof(int) + 3 * (size_t)g.W * p.S * sizeof(unsigned short);
     p.prep_bytes = 6 * plane * sizeof(float);
     p.misc_bytes = 2 * kSumBlocks * sizeof(double) + 256;
@@ -1082,7 +1082,7 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     const dim3 tiles((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2);
     hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2), dim3(256), 0, s, g, a, acc,
                        remT, remT1);
-    hipLaunchKernelGGL(k_bwd_combine2<T>, tiles, dim3(256), lds, s, g, cam, proj, shift, acc, dcam, dproj);
+    hipLaunchKernelGGL(k_bwd_combine2<T>, tiles, dim3(256), lds, s, g, cam, proj, shift, acc, sc, sp, dcam, dproj);
     return hipGetLastError();
 }
 
