@@ -10,8 +10,8 @@ mkdir -p $O
 bash scripts/gpu_tests.sh $TAG -k "backward or bwd or grad or config or rowband or verify" || exit 1
 SPECS=()
 for V in "$@"; do SPECS+=("$V:$V:"); done
-bash scripts/gpu_ab.sh $TAG c5_win bwd 2 "${SPECS[@]}" || exit 1
-bash scripts/gpu_ab.sh $TAG c2_full bwd 2 "${SPECS[@]}" || exit 1
+bash scripts/gpu_ab.sh $TAG/c5 c5_win bwd 2 "${SPECS[@]}" || exit 1
+bash scripts/gpu_ab.sh $TAG/c2 c2_full bwd 2 "${SPECS[@]}" || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 scripts/kbench.py --cfg c5_win --ops bwd --reps 5 > $O/prof.log 2>&1 || { echo "rocprof failed"; tail -10 $O/prof.log; exit 1; }
 python3 - "$O" <<'PY'
 import csv, glob, sys
