@@ -260,33 +260,43 @@ def pmc_child(args):
     torch.cuda.synchronize()
 
 
+def _pmc_pass(args, which, kernel, counters, out):
+    """One rocprofv3 --pmc pass over a child running the op; mean value per `kernel` launch."""
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    d = os.path.join(out, counters[0])
+    cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", *counters, "-d", d, "-o", "run",
+           "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--workload",
+           args.workload, "--precision", args.precision, "--pmc-child", which]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
+    if r.returncode != 0:
+        return None, f"rocprofv3 --pmc {' '.join(counters)} failed (rc {r.returncode}): {r.stderr[-300:]}"
+    xs = {c: [] for c in counters}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] in xs:
+                xs[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    if not all(xs.values()):
+        return None, f"no {counters} samples for {kernel}"
+    return {c: sum(v) / len(v) for c, v in xs.items()}, None
+
+
 def pmc_traffic(args, which, kernel):
     """HBM bytes per launch of `kernel`: two rocprofv3 passes over a child running the op
     (FETCH_SIZE and WRITE_SIZE cannot share a pass; MI355X_MICROARCH.md §HBM/rocprofv3:
-    both in KiB, FETCH_SIZE reports half the bytes on gfx950 -> x2048 and x1024 B/unit)."""
+    both in KiB, FETCH_SIZE reports half the bytes on gfx950 -> x2048 and x1024 B/unit),
+    plus one SQ pass for the instruction mix (wave-instructions per launch)."""
     out = tempfile.mkdtemp(prefix="custma_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     vals = {}
     for counter, scale in (("FETCH_SIZE", 2048.0), ("WRITE_SIZE", 1024.0)):
-        d = os.path.join(out, counter)
-        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", counter, "-d", d, "-o", "run",
-               "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--workload",
-               args.workload, "--precision", args.precision, "--pmc-child", which]
-        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
-        if r.returncode != 0:
-            return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode}): {r.stderr[-300:]}"
-        xs = []
-        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            for row in csv.DictReader(open(f)):
-                if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                    xs.append(float(row["Counter_Value"]))
-        if not xs:
-            return None, f"no {counter} samples for {kernel}"
-        vals[counter] = sum(xs) / len(xs) * scale
-    src = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate) over `bench.py --pmc-child {which}` "
-           f"(same workload), mean per {kernel} launch; FETCH x2048 B, WRITE x1024 B per unit")
+        v, err = _pmc_pass(args, which, kernel, [counter], out)
+        if v is None:
+            return None, err
+        vals[counter] = v[counter] * scale
+    sq, _ = _pmc_pass(args, which, kernel, ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"], out)
+    src = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_* passes (separate) over `bench.py --pmc-child "
+           f"{which}` (same workload), mean per {kernel} launch; FETCH x2048 B, WRITE x1024 B per unit")
     return {"read": vals["FETCH_SIZE"], "write": vals["WRITE_SIZE"],
-            "total": vals["FETCH_SIZE"] + vals["WRITE_SIZE"]}, src
+            "total": vals["FETCH_SIZE"] + vals["WRITE_SIZE"], "sq": sq}, src
 
 
 def main():
@@ -376,23 +386,33 @@ def main():
         elapsed, nvox_all = float(t_max.item()), float(v_sum.item())
     else:
         nvox_all = float(nvox_rank)
+    # distinct GPUs the ranks actually ran on (a gloo rehearsal maps several ranks to one GPU)
+    n_dev = 1
+    if distributed:
+        devs = [None] * world
+        dist.all_gather_object(devs, (socket.gethostname(), torch.cuda.current_device()))
+        n_dev = len(set(devs))
     value = nvox_all * args.steps / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
 
-    # Algorithmic bytes per launch, this rank's band:
-    #   forward sweep  : volume written once + both images read
-    #   backward sweep : upstream gradient + saved volume read once each, both images read,
-    #                    both image gradients written (fp32)
+    # Algorithmic bytes per launch, SURVEY.md §8(d) unit-of-work formulas, this rank's band:
+    #   forward  : N_vox * 4 (volume written) + 2 H W sizeof(image)
+    #   backward : N_vox * 4 (upstream gradient read) + 2 H W sizeof(image) + 2 H W * 4 (both gradients)
+    # The backward's design also re-reads the saved volume (V = A * cost / S):
+    # `design_bytes` adds that N_vox * 4; it is reported beside, never as the roofline figure.
     esz = cam.element_size()
     img = 2 * cam.numel() * esz
     fwd_bytes = nvox_rank * 4 + img
-    bwd_bytes = 2 * nvox_rank * 4 + img + 2 * cam.numel() * 4
+    bwd_bytes = nvox_rank * 4 + img + 2 * cam.numel() * 4
+    bwd_design = bwd_bytes + nvox_rank * 4
     fwd_name = fwd_kernel_name(layout, W, D)
     kern = {
         fwd_name: {"avg_launch_ms": round(fwd_kms, 4), "launches": n_fk, "algorithmic_bytes": fwd_bytes,
                    "achieved_GBps": round(fwd_bytes / (fwd_kms * 1e-3) / 1e9, 1) if fwd_kms else None},
         "k_bwd_coop": {"avg_launch_ms": round(bwd_kms, 4), "launches": n_bk, "algorithmic_bytes": bwd_bytes,
-                       "achieved_GBps": round(bwd_bytes / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None},
+                       "design_bytes": bwd_design,
+                       "achieved_GBps": round(bwd_bytes / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None,
+                       "design_GBps": round(bwd_design / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None},
     }
     dom = "k_bwd_coop" if bwd_kms >= fwd_kms else fwd_name
     dk = kern[dom]
@@ -406,7 +426,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": wl["scaling"],
+        "scaling": wl["scaling"] if n_dev == world else "rehearsal (ranks share GPUs; not a scaling figure)",
         "vs_baseline": None,
         "dtype": "f16" if wl["dtype"] == torch.float16 else "f32",
         "data": "synthetic (seeded speckle pair, camera = shifted projector + noise; uniform upstream grad)",
@@ -414,8 +434,10 @@ def main():
             "workload": wl["desc"],
             "H": global_H, "W": W, "k": k, "D": D, "layout": layout, "precision": args.precision,
             "rows_per_gpu": rows, "voxels_per_step": int(nvox_all),
-            "parallelism": f"rowband{world}" if distributed else "single",
+            "parallelism": (f"rowband{world}" + ("" if n_dev == world else f"-rehearsal-on-{n_dev}-gpu"))
+                           if distributed else "single",
             "dist_backend": args.dist_backend if distributed else None,
+            "distinct_gpus": n_dev,
         },
         "roofline": {
             "bound": "hbm",
@@ -426,6 +448,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": None,
             "algorithmic_bytes_per_launch": dk["algorithmic_bytes"],
+            "algorithmic_formula": ("N_vox*4 + 2*H*W*sizeof(image) + 2*H*W*4 (SURVEY 8(d) backward)"
+                                    if dom == "k_bwd_coop" else "N_vox*4 + 2*H*W*sizeof(image) (SURVEY 8(d) forward)"),
+            "design_bytes_per_launch": dk.get("design_bytes", dk["algorithmic_bytes"]),
             "avg_launch_ms": dk["avg_launch_ms"],
             "timing": "HIP events around each launch of the kernel on the op's stream, over the timed steps",
         },
@@ -443,9 +468,17 @@ def main():
         if not args.no_pmc:
             traffic, src = pmc_traffic(args, "bwd" if dom == "k_bwd_coop" else "fwd", dom)
             if traffic is not None:
-                result["roofline"]["traffic"] = round(traffic["total"])
-                result["roofline"]["traffic_read"] = round(traffic["read"])
-                result["roofline"]["traffic_write"] = round(traffic["write"])
+                rf = result["roofline"]
+                rf["traffic"] = round(traffic["total"])
+                rf["traffic_read"] = round(traffic["read"])
+                rf["traffic_write"] = round(traffic["write"])
+                rf["traffic_over_algorithmic"] = round(traffic["total"] / rf["algorithmic_bytes_per_launch"], 3)
+                rf["traffic_over_design"] = round(traffic["total"] / rf["design_bytes_per_launch"], 3)
+                sq = traffic.get("sq")
+                if sq:
+                    rf["sq_per_launch"] = {k: round(v) for k, v in sq.items()}
+                    rf["valu_wave_insts_per_voxel"] = round(sq["SQ_INSTS_VALU"] / nvox_rank, 4)
+                    rf["valu_lane_ops_per_voxel"] = round(64 * sq["SQ_INSTS_VALU"] / nvox_rank, 2)
             result["roofline"]["traffic_source"] = src
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(wl, args.cpu_rows or (48 if layout == "window" else 96))

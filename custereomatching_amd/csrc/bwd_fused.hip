@@ -40,6 +40,7 @@
 // stores of fp32 partial sums per diagonal chunk; k_bwd_gather sums the
 // chunks and k_bwd_combine applies the box filters.
 #include <algorithm>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -616,29 +617,42 @@ __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, Bwd
 // Per (range class, column): the partial slots that hold the column (class 0 = camera
 // T1c / Am / B, which share one range; 1 = projector T1p; 2 = projector Ac / Bp).
 // cover layout: [3][W] counts, then [3][W][S] slot indices (uint16).
+// cover_column counts every (chunk, segment) whose written range holds column x and stores the
+// first S slot indices into `list` (when given).  plan_bwd's S bounds the count by construction
+// (2 x the max chunk overlap, <= 2 segments per chunk); the host re-checks that for every column
+// (cover_fits), and the device marks an over-full column with count -1, which k_bwd_gather turns
+// into NaN gradients -- never a silently dropped slot.
+__host__ __device__ inline int cover_column(const Geo& g, int64_t dlo, int nChunk, int S, int Sj, int64_t x, int cls,
+                                            unsigned short* list) {
+    const int t = cls == 0 ? 0 : cls == 1 ? 3 : 4;
+    int n = 0;
+    for (int j = 0; j < nChunk; ++j) {
+        const ChunkGeo c = chunk_geo(g, dlo, j);
+        int64_t lo, hi;
+        type_range(c, g.r, t, &lo, &hi);
+        if (x < lo || x >= hi) continue;
+        const int ns = chunk_nseg(c, g.r);
+        // the segment(s) of chunk j whose written range holds column x (<= 2, adjacent)
+        const int64_t rel = x - (c.wlo - g.r) - (cls ? c.d0 : 0);
+        const int sa = (int)(rel >= 0 ? rel / kSeg : -((-rel + kSeg - 1) / kSeg));
+        for (int sg = sa - 1; sg <= sa + 1; ++sg) {
+            if (sg < 0 || sg >= ns) continue;
+            seg_range(c, g.r, sg, t, &lo, &hi);
+            if (x >= lo && x < hi) {
+                if (list && n < S) list[n] = (unsigned short)(2 * (j % Sj) + (sg & 1));
+                ++n;
+            }
+        }
+    }
+    return n;
+}
 __global__ __launch_bounds__(256) void k_bwd_cover(Geo g, int64_t dlo, int nChunk, int S, int Sj, int* cover) {
     const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= g.W) return;
     unsigned short* list = (unsigned short*)(cover + 3 * g.W);
     for (int cls = 0; cls < 3; ++cls) {
-        const int t = cls == 0 ? 0 : cls == 1 ? 3 : 4;
-        int n = 0;
-        for (int j = 0; j < nChunk; ++j) {
-            const ChunkGeo c = chunk_geo(g, dlo, j);
-            int64_t lo, hi;
-            type_range(c, g.r, t, &lo, &hi);
-            if (x < lo || x >= hi) continue;
-            const int ns = chunk_nseg(c, g.r);
-            // the segment(s) of chunk j whose written range holds column x (<= 2, adjacent)
-            const int64_t rel = x - (c.wlo - g.r) - (cls ? c.d0 : 0);
-            const int sa = (int)(rel >= 0 ? rel / kSeg : -((-rel + kSeg - 1) / kSeg));
-            for (int sg = sa - 1; sg <= sa + 1; ++sg) {
-                if (sg < 0 || sg >= ns) continue;
-                seg_range(c, g.r, sg, t, &lo, &hi);
-                if (x >= lo && x < hi && n < S) list[((size_t)cls * g.W + x) * S + n++] = (unsigned short)(2 * (j % Sj) + (sg & 1));
-            }
-        }
-        cover[cls * g.W + x] = n;
+        const int n = cover_column(g, dlo, nChunk, S, Sj, x, cls, list + ((size_t)cls * g.W + x) * S);
+        cover[cls * g.W + x] = n <= S ? n : -1;
     }
 }
 
@@ -652,6 +666,7 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
     const int t = 3 * side + q;
     const int cls = side == 0 ? 0 : (q == 0 ? 1 : 2);
     const int n = a.cover[cls * g.W + x];
+    if (n < 0) return __builtin_nan("");  // more slots than planned (k_bwd_cover): fail loudly
     const unsigned short* sl = list + ((size_t)cls * g.W + x) * a.S;
     const float* base = a.part + (size_t)t * a.S * plane + p;
     double v0 = 0.0, v1 = 0.0;
@@ -890,6 +905,34 @@ struct BwdPlan {
     size_t part_bytes, acc_bytes, cover_bytes, prep_bytes, misc_bytes, rem_bytes;
 };
 
+// Host re-check of the slot bound: every column's cover count <= S (k_bwd_cover's own counting
+// code).  Cached per geometry -- the full layout's check is W x 2W/64 chunk tests.
+bool cover_fits(const Geo& g, int64_t dlo, int nChunk, int S, int Sj) {
+    struct Key {
+        int64_t W, D, dlo;
+        int r, layout, nChunk, S;
+        bool operator==(const Key& o) const {
+            return W == o.W && D == o.D && dlo == o.dlo && r == o.r && layout == o.layout && nChunk == o.nChunk &&
+                   S == o.S;
+        }
+    };
+    static std::mutex mu;
+    static std::vector<Key> good;
+    const Key key{g.W, g.D, dlo, g.r, g.layout, nChunk, S};
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (const Key& k : good)
+            if (k == key) return true;
+    }
+    for (int cls = 0; cls < 3; ++cls)
+        for (int64_t x = 0; x < g.W; ++x)
+            if (cover_column(g, dlo, nChunk, S, Sj, x, cls, nullptr) > S) return false;
+    std::lock_guard<std::mutex> lk(mu);
+    if (good.size() > 256) good.clear();
+    good.push_back(key);
+    return true;
+}
+
 BwdPlan plan_bwd(const Geo& g) {
     BwdPlan p;
     const int r = g.r;
@@ -943,6 +986,7 @@ BwdPlan plan_bwd(const Geo& g) {
     }
     p.Sj = p.S;
     p.S = 2 * p.Sj;
+    if (p.ok && !cover_fits(g, p.dlo, p.nChunk, p.S, p.Sj)) p.ok = false;
     p.nsegMax = 1;
     for (int j = 0; j < p.nChunk; ++j) {
         const int ns = chunk_nseg(chunk_geo(g, p.dlo, j), r);

@@ -78,6 +78,11 @@ class RowBandGroup:
         need = max(self.o, self.a)
         if self.world > 1 and need > 0:
             if H is not None:
+                b0, e0 = band_bounds(H, self.world, self.rank)
+                if n is not None and int(n) != e0 - b0:
+                    raise ValueError(f"rank {self.rank} holds {int(n)} rows but band_bounds({H}, {self.world}, "
+                                     f"{self.rank}) gives {e0 - b0}: pass H=None for a custom row split (the band "
+                                     f"check then runs a MIN all-reduce)")
                 thinnest = min(e - b for b, e in (band_bounds(H, self.world, q) for q in range(self.world)))
             elif n is not None:
                 t = torch.tensor([int(n)], dtype=torch.int64, device=device)
@@ -175,7 +180,7 @@ class _RowBandStereoMatching(torch.autograd.Function):
         ctx.save_for_backward(ch, ph)
         ctx.vol_ref = weakref.ref(vol)
         ctx.vol_version = vol._version
-        ctx.meta = (D, kernel_size, layout, rbg, backend, top, n)
+        ctx.meta = (D, kernel_size, layout, precision, rbg, backend, top, n)
         return vol
 
     @staticmethod
@@ -183,7 +188,9 @@ class _RowBandStereoMatching(torch.autograd.Function):
         ch, ph = ctx.saved_tensors
         vol = ctx.vol_ref()
         vol = vol.detach() if vol is not None and vol._version == ctx.vol_version else None
-        D, k, layout, rbg, backend, top, n = ctx.meta
+        D, k, layout, precision, rbg, backend, top, n = ctx.meta
+        if vol is None:  # dropped or edited in place: recompute with the forward's own arithmetic
+            vol = backend.forward(ch, ph, D, k, layout, precision, (top, top + n))
         want_c, want_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         gc, gp = backend.backward(grad.contiguous(), ch, ph, D, k, layout, (top, top + n), want_c, want_p, vol)
         gc = rbg.reduce_halo(gc, n) if gc is not None else None

@@ -201,6 +201,7 @@ class _StereoMatching(torch.autograd.Function):
         ctx.D = D
         ctx.kernel_size = kernel_size
         ctx.layout = layout
+        ctx.precision = precision or default_precision()
         return vol
 
     @staticmethod
@@ -211,6 +212,12 @@ class _StereoMatching(torch.autograd.Function):
             vol = None  # edited in place after the forward: recompute the costs
         if vol is not None:
             vol = vol.detach()
+        else:
+            # recompute with the forward's own arithmetic, so V = A * cost / S uses the costs the
+            # caller saw (a transient volume-sized buffer during the backward, as the reference's
+            # own backward recomputes its forward per voxel, stereo_matching_kernel.cu:97-128)
+            vol = cost_volume_forward(camera_image, projector_image, ctx.D, ctx.kernel_size, ctx.layout,
+                                      ctx.precision)
         want_c, want_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         gc, gp = cost_volume_backward(cost_volume_grad.contiguous(), camera_image, projector_image,
                                       ctx.kernel_size, ctx.layout, ctx.D, camera_grad=want_c,

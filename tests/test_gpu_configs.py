@@ -17,6 +17,7 @@ import torch
 
 from oracle import oracle as O
 from tests.golden.inputs import make_pair
+from tests.oracle_tiles import tile_backward as _tile_backward
 
 import custereomatching_amd as cm
 
@@ -190,6 +191,20 @@ def test_config4_window_fp16_one_gpu(gpu):
     ex = cm.cost_volume_forward(c[:512].contiguous(), p[:512].contiguous(), D, k, "window", "exact")
     vi, vb = cm.volume_argmax(ex)
     assert torch.equal(idx, vi) and torch.equal(best, vb)
+    del ex, vi, vb
+    # the bench's own step: backward of both images at 4096x8192 from the forward's 33.4 GB volume
+    # (volume offsets past 2^32 bytes), checked on haloed oracle tiles (rows x columns)
+    gen = torch.Generator(device=gpu).manual_seed(102)
+    g = torch.randn(fa.shape, generator=gen, device=gpu)
+    gc, gp = cm.cost_volume_backward(g, c, p, k, "window", D, projector_grad=True, cost_volume=fa)
+    for h0 in (2049, 4090):
+        for c0 in (0, W - 768):
+            h1 = min(H, h0 + 6)
+            rc, rp, (xc0, xc1), (xp0, xp1) = _tile_backward(g, c32, p32, k, D, h0, h1, c0, 768)
+            assert _rel(gc[h0:h1, xc0:xc1].cpu().numpy(), rc) <= 1e-5, (h0, c0)
+            assert _rel(gp[h0:h1, xp0:xp1].cpu().numpy(), rp) <= 1e-5, (h0, c0)
+    assert torch.isfinite(gc).all() and torch.isfinite(gp).all()
+
 
 
 # ---------------- kernel sizes beyond the fused instantiations (generic paths) ----------------

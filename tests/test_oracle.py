@@ -182,3 +182,21 @@ def test_torch_ref_window_layout_matches_c_oracle(k, D, row_chunk):
         assert np.abs(v.numpy() - O.forward_f64(cam, proj, k, layout=O.WINDOW, D=D)).max() <= 1e-9
     assert np.abs(gc.numpy() - rc).max() <= 1e-9 * max(1.0, np.abs(rc).max())
     assert np.abs(gp.numpy() - rp).max() <= 1e-9 * max(1.0, np.abs(rp).max())
+
+
+def test_tile_backward_crop_is_exact():
+    """tests/oracle_tiles.tile_backward (the C5 backward check's oracle) equals the whole-image
+    fp64 oracle on the tile it returns, at both image edges and in the middle."""
+    from tests.golden.inputs import make_pair
+    from tests.oracle_tiles import tile_backward
+
+    H, W, k, D = 20, 150, 5, 24
+    cam, proj = make_pair(H, W, D, seed=9)
+    g = np.random.default_rng(10).standard_normal((H, W - D, D + 1)).astype(np.float32)
+    rc, rp = O.backward_f64(g, cam, proj, k, layout=O.WINDOW, D=D)
+    for h0, c0 in ((0, 0), (7, 30), (15, W - 100)):
+        h1 = min(H, h0 + 4)
+        tc, tp, (a, b), (c, d) = tile_backward(g, cam, proj, k, D, h0, h1, c0, 100)
+        assert b > a and d > c
+        np.testing.assert_allclose(tc, rc[h0:h1, a:b], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(tp, rp[h0:h1, c:d], rtol=0, atol=1e-9)
