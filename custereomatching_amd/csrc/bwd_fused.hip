@@ -41,6 +41,7 @@
 // chunks and k_bwd_combine applies the box filters.
 #include <algorithm>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -58,7 +59,12 @@ namespace {
 constexpr int TRB = CUSTMA_BWD_ROWS;  // own rows per unit (workgroup)
 constexpr int NLB = 64;   // diagonals per wave
 constexpr int NTYPE = 6;  // partial types: T1c, Am, B (camera) | T1p, Ac, Bp (projector)
-constexpr int kSeg = 128; // pixel columns per wave (>= 64 + 2 r: segments s and s+2 never overlap)
+#ifndef CUSTMA_BWD_SEG
+#define CUSTMA_BWD_SEG 512  // 128 -> 512: C5 window backward 28.9 -> 27.6-28.0 ms, C2 full 3.57 -> 3.38 ms (profiles/r03/seg_ab.txt)
+#endif
+// pixel columns per unit (>= 64 + 2 r: segments s and s+2 never overlap); a unit sweeps kSeg + 2 r
+// columns, so the 2 r halo steps are 2 r / kSeg of redundant work
+constexpr int kSeg = CUSTMA_BWD_SEG;
 constexpr uint32_t kOOB = 0x80000000u;
 #ifndef CUSTMA_BWD_PF
 #define CUSTMA_BWD_PF 2
@@ -133,6 +139,12 @@ struct BwdArgs {
     const float* vol;
     const float* shift;  // [2]: cbar, pbar
     float* part;         // [NTYPE][S][H][W]
+    // window layouts with D = 64 n (BwdPlan::rem): the remainder diagonal D's terms, written by the
+    // remainder units (bwd_rem_body), added by k_bwd_gather:
+    //   remT [4][HV][WO]       A mp'(h, w+D), V Y(h, w+D), A mc'(h, w), V X(h, w)
+    //   remT1[2][yhi-ylo][W]   T1c at (y, x): p'(y, x+D) BoxA_D(y, x);  T1p at (y, x+D): c'(y, x) BoxA_D(y, x)
+    float* remT;
+    float* remT1;
     const int* cover;    // k_bwd_cover: slot counts and lists per (range class, column)
     int S, Sj, nChunk, nRG, jc, nsegMax;
     int order;  // block order of k_bwd_coop (see there)
@@ -179,11 +191,16 @@ constexpr int BDP = CUSTMA_BWD_DEPTH;  // steps of loads in flight (1 or 2)
 constexpr bool SLIDE = CUSTMA_BWD_SLIDE;
 // steps per flush (small buffers: 3 workgroups per CU at k = 9); a multiple of BDP + 1, so
 // every flush block starts on load buffer 0
-#ifndef CUSTMA_BWD_FBC
-#define CUSTMA_BWD_FBC (BDP == 2 ? 6 : 8)
+// 16 steps per flush (all 64 lanes store: 4 rows x 16 steps) where the LDS allows it: C5 window
+// backward op 27.7 -> 26.7 ms, C3 3.26 -> 3.19 ms (profiles/r03/win_fbc_ab.txt).  k <= 9 keeps 8, so
+// its 3 workgroups per CU still fit.
+#ifdef CUSTMA_BWD_FBC
+template <int K>
+constexpr int fbc_for() { return CUSTMA_BWD_FBC; }
+#else
+template <int K>
+constexpr int fbc_for() { return BDP == 2 ? 6 : K >= 11 ? 16 : 8; }
 #endif
-constexpr int FBC = CUSTMA_BWD_FBC;
-static_assert(FBC % (BDP + 1) == 0 && FBC <= 16, "flush blocks start on load buffer 0; 4 FBC lanes");
 // A rows of the unit: double-buffered (one barrier per step) or single (a second barrier
 // before the next step's writes; 6.5 KB less LDS at k = 11)
 #ifndef CUSTMA_BWD_ABUF
@@ -201,10 +218,25 @@ __device__ __forceinline__ float reduce_tail3(float w0, float w1, float w2, int 
     return z + dpp<kQuad1032>(z);
 }
 
-template <int K>
+// Window-layout form (WIN): a step's gradient / volume / camera addresses are a per-lane loop
+// constant plus a wave-uniform part, so the step adds the wave-uniform part as the SGPR soffset
+// (SALU) instead of recomputing every lane's offset and bounds (VALU).  Out-of-range markers are
+// kWinNR (>= the window descriptors' num_records, so any one of them is out of range, and any sum
+// of three stays below 2^32); in-range offsets stay below kWinNR (win_path_ok).
+constexpr uint32_t kWinNR = 0x55555550u;
+
+template <int N>
+__device__ __forceinline__ float tree_sum(const float* c) {
+    if constexpr (N == 1) return c[0];
+    else return tree_sum<N / 2>(c) + tree_sum<N - N / 2>(c + N / 2);
+}
+
+template <int K, bool WIN>
 __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, int j, int sg, int rg, float* Abuf,
                                               float* ring, float (*cbuf)[12], float (*pbuf)[12]) {
     constexpr int R = K / 2, NY = TRB + 2 * R, NH = 2 * R;  // NH halo rows
+    constexpr int FBC = fbc_for<K>();
+    static_assert(FBC % (BDP + 1) == 0 && FBC <= 16, "flush blocks start on load buffer 0; 4 FBC lanes");
     constexpr int HPW = (NH + NWC - 1) / NWC;                // halo rows per wave (at most)
     static_assert(HPW <= 4, "a wave's halo rows fit one quad of a 16-lane row");
 
@@ -240,6 +272,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     const auto rV = make_rsrc(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
     const int64_t ir0 = y0 - R;
     const uint32_t vstride = (uint32_t)(slab * 4);
+    const uint32_t vNR = WIN ? kWinNR : 0x7FFFFFF0u;  // the volume descriptors' num_records
     const int hlo = (int)g.h_lo, hhi = (int)g.h_hi, vrow0i = (int)vrow0;
     // The six prepared images are one array (k_bwd_prep: X, mc', c, Y, mp', p) read through ONE
     // descriptor, the image selected by a per-lane offset: two descriptors instead of eight keep
@@ -322,7 +355,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     };
     auto vso = [&](int y) -> uint32_t {
         const int row = (int)ir0 + y;
-        return (row >= hlo && row < hhi) ? (uint32_t)(row - vrow0i) * vstride : 0x7FFFFFF0u;
+        return (row >= hlo && row < hhi) ? (uint32_t)(row - vrow0i) * vstride : vNR;
     };
     uint32_t sIo[TRW], sVo[TRW], sIh[HP], sVh[HP];
 #pragma unroll
@@ -335,11 +368,15 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         const int q = wv + NWC * i;
         const int y = halo_row(q < NH ? q : 0);
         sIh[i] = __builtin_amdgcn_readfirstlane(iso(y));
-        sVh[i] = __builtin_amdgcn_readfirstlane(vso(y));
+        // WIN: a wave without this halo row reads it out of range (its soffset is the marker)
+        sVh[i] = __builtin_amdgcn_readfirstlane(WIN && q >= NH ? vNR : vso(y));
     }
-    const i32x4 dG = make_rsrc_sgpr(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
-    const i32x4 dV = make_rsrc_sgpr(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
+    const i32x4 dG = make_rsrc_sgpr(a.grad + (size_t)(vrow0 - g.h_lo) * slab, vNR);
+    const i32x4 dV = make_rsrc_sgpr(a.vol + (size_t)(vrow0 - g.h_lo) * slab, vNR);
     const i32x4 dPr = make_rsrc_sgpr(a.Xc, 6u * ib);  // a.Xc = the prepared array's base
+    // WIN: the camera-value loads through a descriptor whose range is the marker bound (offsets
+    // stay inside the prepared array: rows checked per lane, columns per step)
+    const i32x4 dPc = make_rsrc_sgpr(a.Xc, kWinNR);
     const int orow_l = y0i + yw + (lane & 3);  // own image row of this lane's quad slot
     int hrow_l = -1;                           // halo image row of this lane's quad slot (or none)
     if ((lane & 3) < HPW && wv + NWC * (lane & 3) < NH) hrow_l = (int)ir0 + halo_row(wv + NWC * (lane & 3));
@@ -351,9 +388,31 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     // NOP: open each load group with `s_nop 4` (VALU SGPR write -> VMEM read); the in-loop
     // issues go without -- their descriptors / soffsets are loop constants, written (by
     // readfirstlane) only in the prologue, which custereomatching_amd/hazard_check.py checks at build time
+    // WIN per-lane loop constants: the lane's diagonal (or the marker past D) and its camera-value
+    // offsets (own row / halo row of its quad slot, each prepared array; the marker outside the image)
+    const uint32_t vLane = dl <= g.D ? (uint32_t)dl * 4u : kWinNR;
+    auto img_row_a = [&](int row, int arr) -> uint32_t {
+        return (row >= 0 && row < Hi) ? (uint32_t)(row * Wi * 4) + arr * pb4 : kWinNR;
+    };
+    const uint32_t vXo = img_row_a(orow_l, kX), vXh = hrow_l >= 0 ? img_row_a(hrow_l, kX) : kWinNR;
+    const uint32_t vMo = img_row_a(orow_l, kMc), vCo = img_row_a(orow_l, kC);
+    const uint32_t gsU4 = (uint32_t)gsU * 4u;
     auto issue = [&](int w, Ld& b, auto nop_) {
         constexpr bool NOP = decltype(nop_)::value;
         const int xb = w - R;
+        if constexpr (WIN) {
+            // wave-uniform parts: the step's volume column (marker outside [0, WO)) and the two
+            // camera columns w and w - R (marker outside [0, W))
+            const uint32_t sW = (w >= 0 && w < (int)g.WO) ? (uint32_t)w * gsU4 : kWinNR;
+            const uint32_t sC = (w >= 0 && w < Wi) ? (uint32_t)w * 4u : kWinNR;
+            const uint32_t sX = (xb >= 0 && xb < Wi) ? (uint32_t)xb * 4u : kWinNR;
+#pragma unroll
+            for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], vLane, vLane, dG, dV, sVo[m] + sW, sVo[m] + sW);
+#pragma unroll
+            for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], vLane, dG, sVh[i] + sW);
+            asm_ld4s<NOP>(b.xo, b.xh, b.mc, b.cx, vXo, vXh, vMo, vCo, dPc, sC, sX);
+            return;
+        }
         const bool ve = w >= lwlo && w < lwhi;
 #ifdef CUSTMA_ABL_BWD_NOMEM  // ablation (timing only): no gradient / volume traffic
         const uint32_t oGe = kOOB + 0 * ve;
@@ -448,7 +507,14 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             if (!flushed || s >= 2 || (SLIDE && s == 1)) asm_vmcnt<NL>();
             else if (s == 1) asm_vmcnt<NL + SF>();
         } else {
+#ifdef CUSTMA_BWD_WAIT0
             asm_vmcnt<0>();
+#else
+            // the step's loads, not the flush's SF stores issued after them (a store's completion
+            // is not needed here; vmcnt counts loads and stores in issue order)
+            if (flushed && s == 0) asm_vmcnt<SF>();
+            else asm_vmcnt<0>();
+#endif
         }
         tie(cur);
         if constexpr (SLIDE) {
@@ -507,9 +573,13 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         float col[TRW + 2 * R];
 #pragma unroll
         for (int y = 0; y < TRW + 2 * R; ++y) col[y] = Acur[(yw + y) * 64 + lane];
+#ifdef CUSTMA_BWD_VSEQ
         float v = 0.f;
 #pragma unroll
         for (int y = 0; y <= 2 * R; ++y) v += col[y];
+#else
+        float v = tree_sum<2 * R + 1>(col);  // a pairwise tree: depth log2(k) instead of a k-long chain
+#endif
         float t1v[TRW];
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
@@ -570,12 +640,149 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     }
 }
 
+// The remainder diagonal D of a window with D = 64 n (BwdPlan::rem): its voxels (h, w, D) are the
+// float right after the last chunk's 64 in every volume row.  They run as an extra chunk rank of
+// units (k_bwd_coop, j == nChunk) dispatched with the full chunks of the same (row group, segment),
+// so their lines are the ones those units are reading (L2 hits; a separate pass reads one
+// 128-byte line per voxel).  A remainder unit is cheap: lanes 0..3 of wave v take its own rows
+// 4v .. 4v+3 and lanes 4.. its share of the halo rows; A_D goes to a small LDS row array (one
+// barrier per step), the own rows' vertical box is a DPP window sum over those lanes, the
+// horizontal box slides through a K-deep LDS ring, and the six terms of each own row go through
+// an LDS buffer to coalesced-per-row stores every FBC steps (a.remT / a.remT1, added by
+// k_bwd_gather).  Same fp32 arithmetic as the sweep.
+template <int K>
+__device__ __forceinline__ void bwd_rem_body(const Geo& g, const BwdArgs& a, int sg, int rg, float* AbufD,
+                                             float* ringD, float (*remb)[4][6]) {
+    constexpr int R = K / 2, NY = TRB + 2 * R, NH = 2 * R;
+    constexpr int FBC = fbc_for<K>();
+    constexpr int HPW = (NH + NWC - 1) / NWC;
+    static_assert(TRW + HPW <= 16, "the rows of a wave fit one 16-lane DPP row");
+    const ChunkGeo cg = chunk_geo(g, a.dlo, 0);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int Wi = (int)g.W, Hi = (int)g.H, WOi = (int)g.WO, Di = (int)g.D;
+    const int64_t y0 = a.ylo + (int64_t)TRB * rg;
+    const int y0i = (int)y0, ir0 = y0i - R;
+    int64_t xs64, xe64;
+    seg_cols(cg, R, sg, &xs64, &xe64);
+    const int xs = (int)xs64, xe = (int)xe64, w0 = xs - R, wend = xe + R;
+    const int yw = TRW * wv;
+    const int hlo = (int)g.h_lo, hhi = (int)g.h_hi;
+    const size_t slab = (size_t)g.WO * g.DO, plane = (size_t)g.H * g.W;
+    const int64_t vrow0 = max(g.h_lo, y0 - R);
+    const int vrow0i = (int)vrow0;
+    const uint32_t vstride = (uint32_t)(slab * 4), pb4 = (uint32_t)(plane * 4);
+    const float cb = a.shift[0], pb = a.shift[1];
+    enum { kX = 0, kMc = 1, kC = 2, kY = 3, kMp = 4, kP = 5 };
+    // this lane's row (unit row index) and its offsets (kWinNR: none / outside)
+    int row = -1;
+    if (lane < TRW) row = R + yw + lane;
+    else if (lane < TRW + HPW && wv + NWC * (lane - TRW) < NH) {
+        const int q = wv + NWC * (lane - TRW);
+        row = q < R ? q : q + TRB;
+    }
+    const int img = row >= 0 ? ir0 + row : -1;
+    auto img_row_a = [&](int arr) -> uint32_t {
+        return (row >= 0 && img >= 0 && img < Hi) ? (uint32_t)(img * Wi * 4) + arr * pb4 : kWinNR;
+    };
+    const bool own = lane < TRW;
+    const uint32_t vG = (row >= 0 && img >= hlo && img < hhi) ? (uint32_t)(img - vrow0i) * vstride + (uint32_t)Di * 4u
+                                                              : kWinNR;
+    const uint32_t vX = img_row_a(kX), vY = img_row_a(kY) == kWinNR ? kWinNR : img_row_a(kY) + (uint32_t)Di * 4u;
+    const uint32_t vMc = own ? img_row_a(kMc) : kWinNR, vC = own ? img_row_a(kC) : kWinNR;
+    const uint32_t vMp = own && img_row_a(kMp) != kWinNR ? img_row_a(kMp) + (uint32_t)Di * 4u : kWinNR;
+    const uint32_t vP = own ? img_row_a(kP) : kWinNR;
+    const auto rG = make_rsrc(a.grad + (size_t)(vrow0 - g.h_lo) * slab, kWinNR);
+    const auto rV = make_rsrc(a.vol + (size_t)(vrow0 - g.h_lo) * slab, kWinNR);
+    const auto rP = make_rsrc(a.Xc, kWinNR);
+    const uint32_t gsU4 = (uint32_t)g.DO * 4u;
+    struct Ld { float g, v, x, y, mp, mc, c, p; };
+    auto load = [&](int w, Ld& b) {
+        const int xb = w - R, xd = xb + Di;
+        const bool wv_ok = w >= 0 && w < WOi;  // volume column (and projector column w + D < W)
+        const uint32_t sW = wv_ok ? (uint32_t)w * gsU4 : kWinNR;
+        const uint32_t sC = (w >= 0 && w < Wi) ? (uint32_t)w * 4u : kWinNR;
+        const uint32_t sCD = wv_ok ? (uint32_t)w * 4u : kWinNR;
+        const uint32_t sX = (xb >= 0 && xb < Wi) ? (uint32_t)xb * 4u : kWinNR;
+        const uint32_t sXD = (xd >= 0 && xd < Wi) ? (uint32_t)xd * 4u : kWinNR;
+        b.g = ld_bufs<float>(rG, vG, sW);
+        b.v = ld_bufs<float>(rV, vG, sW);
+        b.x = ld_bufs<float>(rP, vX, sC);
+        b.y = ld_bufs<float>(rP, vY, sCD);
+        b.mp = ld_bufs<float>(rP, vMp, sCD);
+        b.mc = ld_bufs<float>(rP, vMc, sC);
+        b.c = ld_bufs<float>(rP, vC, sX);
+        b.p = ld_bufs<float>(rP, vP, sXD);
+    };
+    const int64_t nvR = g.HV() * g.WO, nywR = (a.yhi - a.ylo) * g.W;
+    const auto rT = make_rsrc(a.remT, (uint32_t)(4 * nvR * 4));
+    const auto rT1 = make_rsrc(a.remT1, (uint32_t)(2 * nywR * 4));
+    if (own)
+#pragma unroll
+        for (int s2 = 0; s2 < K; ++s2) ringD[s2 * TRW + lane] = 0.f;
+    float HVD = 0.f;
+    int sidx = 0;
+    Ld cur, nxt;
+    load(w0, cur);
+    for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
+        const int nsteps = min(FBC, wend - wfirst);
+        for (int s = 0; s < nsteps; ++s) {
+            const int w = wfirst + s;
+            load(w + 1, nxt);  // past the segment's end: in range or masked, never used
+            const float rSD = __builtin_amdgcn_rsqf(__builtin_fmaf(cur.x, cur.y, kEps));
+            const float AD = cur.g * rSD;
+            float* AbD = AbufD + ((w - w0) & 1) * NY;
+            if (row >= 0) AbD[row] = AD;
+            const float VD = AD * cur.v * rSD;
+            const float rsvD = ringD[sidx * TRW + (lane & (TRW - 1))];
+            __syncthreads();  // the unit's A_D of this step is published (double-buffered)
+            const float xD = lane < TRW + 2 * R ? AbD[yw + lane] : 0.f;
+            float vD = xD;  // lane m: unit rows yw + m .. yw + m + 2R (lanes m .. m + 2R)
+            if constexpr (TRW - 1 + 2 * R < 16) {
+                Unroll<1, 2 * R + 1>::run([&](auto ic) { vD += dpp<0x100 + decltype(ic)::value>(xD); });  // row_shl
+            } else {
+#pragma unroll
+                for (int i = 1; i <= 2 * R; ++i) vD += AbD[yw + (lane & (TRW - 1)) + i];
+            }
+            HVD += vD - rsvD;
+            if (own) {
+                ringD[sidx * TRW + lane] = vD;
+                float* rb = remb[s][lane];
+                rb[0] = AD * cur.mp;               // camera Am at (row, w):  A mp'(row, w + D)
+                rb[1] = VD * cur.y;                // camera B  at (row, w):  V Y(row, w + D)
+                rb[2] = AD * cur.mc;               // projector Ac at (row, w + D): A mc'(row, w)
+                rb[3] = VD * cur.x;                // projector Bp at (row, w + D): V X(row, w)
+                rb[4] = (cur.p - pb) * HVD;        // T1c at (row, xb): p'(row, xb + D) BoxA_D
+                rb[5] = (cur.c - cb) * HVD;        // T1p at (row, xb + D): c'(row, xb) BoxA_D
+            }
+            sidx = sidx + 1 == K ? 0 : sidx + 1;
+            cur = nxt;
+        }
+        // flush: lane (jcol, m) stores the six terms of step wfirst + jcol, own row m
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int jcol = ln % FBC, m = (ln / FBC) & 3;
+        const bool live = jcol < nsteps && ln < 4 * FBC;
+        const int w = wfirst + jcol, x = w - R, y = y0i + yw + m;
+        const float* rv = remb[jcol][m];
+        const bool wok = live && w >= xs && w < xe && w >= 0 && w < WOi && y >= hlo && y < hhi;
+        const uint32_t tv = (uint32_t)(((y - hlo) * WOi + w) * 4), tn = (uint32_t)(nvR * 4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) st_buf(rv[t], rT, wok ? tv + t * tn : kOOB);
+        const bool xok = live && x >= xs && x < xe && y < (int)a.yhi;
+        const uint32_t ty = (uint32_t)((y - (int)a.ylo) * Wi * 4);
+        st_buf(rv[4], rT1, (xok && x >= 0 && x < Wi) ? ty + (uint32_t)(x * 4) : kOOB);
+        const int o = x + Di;
+        st_buf(rv[5], rT1, (xok && o >= 0 && o < Wi) ? (uint32_t)(nywR * 4) + ty + (uint32_t)(o * 4) : kOOB);
+    }
+}
+
 #ifdef CUSTMA_BWD_WPE
 #define CUSTMA_BWD_OCC __attribute__((amdgpu_waves_per_eu(CUSTMA_BWD_WPE)))
 #else
 #define CUSTMA_BWD_OCC
 #endif
-template <int K>
+template <int K, bool WIN, bool REM>
 __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, BwdArgs a) {
     // XCD x owns row groups [x nRGx, (x+1) nRGx) (their halo rows are read on one XCD).
     // A wave's 256-byte gradient / volume row segment spans three 128-byte lines whose outer
@@ -586,32 +793,45 @@ __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, Bwd
     //   FETCH 140 -> 103 GB per launch, 37.1 -> 35.7 ms op).
     // a.order 1 (full layout, up to 2W/64 chunks of very different lengths): row group fastest,
     //   then chunk rank (longest first), then segment (C2 full: 4.36 -> 3.85-4.05 ms op).
+    // REM: one more chunk rank, j == nChunk: the remainder diagonal's units (bwd_rem_body)
     const int64_t hb = blockIdx.x, xi = hb / 8, x = hb % 8;
     const int nRGx = (a.nRG + 7) / 8;
+    const int nU = a.nChunk + (REM ? 1 : 0);
     int j, sg, rg;
     if (a.order == 2) {
-        const int jr = (int)(xi % a.nChunk);
-        const int64_t rest = xi / a.nChunk;
+        const int jr = (int)(xi % nU);
+        const int64_t rest = xi / nU;
         rg = (int)(x * nRGx + rest % nRGx);
         const int64_t sg64 = rest / nRGx;
         if (rg >= a.nRG || sg64 >= a.nsegMax) return;
-        j = chunk_of_rank(jr, a.nChunk, a.jc);
+        j = REM && jr == a.nChunk ? jr : chunk_of_rank(jr, a.nChunk, a.jc);
         sg = (int)sg64;
     } else {
         const int64_t unit = xi / nRGx;
         rg = (int)(x * nRGx + xi % nRGx);
-        if (rg >= a.nRG || unit >= (int64_t)a.nChunk * a.nsegMax) return;
-        j = chunk_of_rank((int)(unit % a.nChunk), a.nChunk, a.jc);
-        sg = (int)(unit / a.nChunk);
+        if (rg >= a.nRG || unit >= (int64_t)nU * a.nsegMax) return;
+        const int jr = (int)(unit % nU);
+        j = REM && jr == a.nChunk ? jr : chunk_of_rank(jr, a.nChunk, a.jc);
+        sg = (int)(unit / nU);
     }
-    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
+    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, REM && j == a.nChunk ? 0 : j), g.r)) return;
     constexpr int NY = TRB + 2 * (K / 2);
     __shared__ __attribute__((aligned(16))) float Abuf[NAB * NY * 64];
     __shared__ __attribute__((aligned(16))) float ring[NWC * K * TRW * 64];
+    constexpr int FBC = fbc_for<K>();
     __shared__ __attribute__((aligned(16))) float cbuf[NWC][FBC][12];
     __shared__ __attribute__((aligned(16))) float pbuf[NWC][FBC][12];
     const int wv = threadIdx.x >> 6;
-    bwd_coop_body<K>(g, a, j, sg, rg, Abuf, ring + wv * (K * TRW * 64), cbuf[wv], pbuf[wv]);
+    if constexpr (REM) {
+        if (j == a.nChunk) {  // the remainder diagonal's unit: its small buffers alias the sweep's
+            float* AbufD = Abuf;                                         // [2][NY]
+            float* ringD = ring + 2 * NY + wv * (K * TRW);               // [NWC][K][TRW]
+            float(*remb)[4][6] = (float(*)[4][6])(ring + 2 * NY + NWC * K * TRW) + wv * FBC;  // [NWC][FBC][4][6]
+            bwd_rem_body<K>(g, a, sg, rg, AbufD, ringD, remb);
+            return;
+        }
+    }
+    bwd_coop_body<K, WIN>(g, a, j, sg, rg, Abuf, ring + wv * (K * TRW * 64), cbuf[wv], pbuf[wv]);
 }
 
 // Per (range class, column): the partial slots that hold the column (class 0 = camera
@@ -658,8 +878,8 @@ __global__ __launch_bounds__(256) void k_bwd_cover(Geo g, int64_t dlo, int nChun
 
 // Sum of the partial slots of type 3 side + q at pixel p = (y, x) (fp64, even / odd slots in two
 // accumulators, in the cover list's order), plus the remainder diagonal's term of that type
-// (k_bwd_rem_*).  The caller checks y in [ylo, yhi).
-__device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, const float* remT, const double* remT1,
+// (BwdArgs::remT / remT1, written by the last chunk's units).  The caller checks y in [ylo, yhi).
+__device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, const float* remT, const float* remT1,
                                              int side, int q, int64_t y, int64_t x, int64_t p) {
     const int64_t plane = g.H * g.W;
     const unsigned short* list = (const unsigned short*)(a.cover + 3 * g.W);
@@ -677,10 +897,12 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
     }
     if (i < n) v0 += (double)base[(size_t)sl[i] * plane];
     double s = v0 + v1;
-    if (remT) {  // the remainder diagonal's terms (k_bwd_rem_*)
+    if (remT) {  // the remainder diagonal's terms (bwd_rem_body)
         const int64_t nyw = (a.yhi - a.ylo) * g.W, nv = g.HV() * g.WO, yy = y - a.ylo, D = g.D;
         if (q == 0) {
-            if (side == 0 || x >= D - g.r) s += remT1[side * nyw + yy * g.W + x];
+            // written for camera columns x < WO + r (past them the box of diagonal D is empty) and
+            // projector columns o >= D - r
+            if (side == 0 ? x < g.WO + g.r : x >= D - g.r) s += (double)remT1[side * nyw + yy * g.W + x];
         } else {
             const int64_t w = side == 0 ? x : x - D;  // the voxel column of this pixel on diagonal D
             if (y >= g.h_lo && y < g.h_hi && w >= 0 && w < g.WO)
@@ -690,11 +912,20 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
     return s;
 }
 
-// Sum the partial slots per pixel; out (fp64, [2 sides][3][H][W]): T1, Am|Ac, B|Bp (k_bwd_combine2
+// Per-pixel sums (k_bwd_gather -> k_bwd_combine2): fp64 sums of the fp32 chunk partials, stored as
+// fp32 (one more rounding of values that are sums of fp32 partials already; the box filters and the
+// final combination stay fp64).  CUSTMA_BWD_ACC64: fp64 storage (benchmarking / checking only).
+#ifdef CUSTMA_BWD_ACC64
+typedef double acc_t;
+#else
+typedef float acc_t;
+#endif
+
+// Sum the partial slots per pixel; out ([2 sides][3][H][W]): T1, Am|Ac, B|Bp (k_bwd_combine2
 // forms m' B as it loads its tile -- the same product, one fp64 array less through HBM).
 template <typename T>
-__global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* acc, const float* remT,
-                                                    const double* remT1) {
+__global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, acc_t* acc, const float* remT,
+                                                    const float* remT1) {
     // blockIdx.y = the image row, x = the column, z = the side (no 64-bit division per thread)
     const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     const int64_t plane = g.H * g.W;
@@ -706,16 +937,16 @@ __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, double* ac
 #pragma unroll
         for (int q = 0; q < 3; ++q) s[q] = gather_sum(g, a, remT, remT1, side, q, y, x, p);
     }
-    double* o = acc + (size_t)side * 3 * plane;
-    o[p] = s[0];
-    o[plane + p] = s[1];
-    o[2 * plane + p] = s[2];
+    acc_t* o = acc + (size_t)side * 3 * plane;
+    o[p] = (acc_t)s[0];
+    o[plane + p] = (acc_t)s[1];
+    o[2 * plane + p] = (acc_t)s[2];
 }
 
 // grad(y,x) = T1 - Box[A] - img'(y,x) Box[B] + Box[m' B]   (one side per blockIdx.z)
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict__ cam, const T* __restrict__ proj,
-                                                      const float* __restrict__ shift, const double* __restrict__ acc,
+                                                      const float* __restrict__ shift, const acc_t* __restrict__ acc,
                                                       Stats sc, Stats sp, float* __restrict__ dcam,
                                                       float* __restrict__ dproj) {
     constexpr int TS = 16;
@@ -725,9 +956,9 @@ __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict
     if (!out) return;
     const T* img = side == 0 ? cam : proj;
     const int64_t plane = g.H * g.W;
-    const double* T1 = acc + (size_t)side * 3 * plane;
-    const double* Aa = T1 + plane;
-    const double* Bb = Aa + plane;
+    const acc_t* T1 = acc + (size_t)side * 3 * plane;
+    const acc_t* Aa = T1 + plane;
+    const acc_t* Bb = Aa + plane;
     const double* box = side == 0 ? sc.box : sp.box;
     const double sh = (double)shift[side], rk2 = (double)(g.k * g.k);
     const int r = g.r, L = TS + 2 * r;
@@ -776,23 +1007,37 @@ __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict
     }
     const int64_t q = y * g.W + x;
     const double ip = (double)to_f(img[q]) - (double)shift[side];
-    out[q] = (float)(T1[q] - sa - ip * sb + sm);
+    out[q] = (float)((double)T1[q] - sa - ip * sb + sm);
 }
 
-// Image means (the global shifts cbar, pbar): per-block fp64 sums, then one block.
+// Image means (the global shifts cbar, pbar): per-block fp64 sums (blockIdx.y = the image; four
+// independent loads in flight per thread -- one dependent load at a time left this HBM-latency
+// bound: 103 us per image at 4096 x 8192), then one block.
 template <typename T>
-__global__ __launch_bounds__(256) void k_img_blocksum(const T* __restrict__ img, int64_t n, double* bsum) {
+__global__ __launch_bounds__(256) void k_img_blocksum(const T* __restrict__ img0, const T* __restrict__ img1,
+                                                      int64_t n, double* bsum) {
     __shared__ double red[256];
-    double v = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-        v += (double)to_f(img[i]);
+    const T* __restrict__ img = blockIdx.y ? img1 : img0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const float a = to_f(img[i]), b = to_f(img[i + stride]), c = to_f(img[i + 2 * stride]),
+                    d = to_f(img[i + 3 * stride]);
+        v0 += (double)a;
+        v1 += (double)b;
+        v2 += (double)c;
+        v3 += (double)d;
+    }
+    for (; i < n; i += stride) v0 += (double)to_f(img[i]);
+    double v = (v0 + v1) + (v2 + v3);
     red[threadIdx.x] = v;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
         if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
         __syncthreads();
     }
-    if (threadIdx.x == 0) bsum[blockIdx.x] = red[0];
+    if (threadIdx.x == 0) bsum[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
 }
 __global__ __launch_bounds__(256) void k_img_shift(const double* __restrict__ bsum, int nb, int64_t n, float* shift) {
     __shared__ double red[256];
@@ -810,88 +1055,10 @@ __global__ __launch_bounds__(256) void k_img_shift(const double* __restrict__ bs
     }
 }
 
-// fp32 images for the sweep (after the shifts are known): X = camera centred moment,
-// mc' = camera patch mean - cbar, c = camera; Y, mp', p likewise for the projector.  The
-// images stay unshifted so that a zero-padded (out-of-image) load minus the shift gives the
-// shifted padding value -cbar / -pbar.
-template <typename T>
-__global__ __launch_bounds__(256) void k_bwd_prep(Geo g, const T* __restrict__ cam, const T* __restrict__ proj,
-                                                  Stats sc, Stats sp, const float* __restrict__ shift, float* prep) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t plane = g.H * g.W;
-    if (p >= plane) return;
-    const double rk2 = 1.0 / (double)(g.k * g.k);
-    const float cb = shift[0], pb = shift[1];
-    prep[p] = sc.sqt[p];
-    prep[plane + p] = (float)(sc.box[p] * rk2 - (double)cb);
-    prep[2 * plane + p] = to_f(cam[p]);  // raw: the sweep subtracts cbar after a zero-padded load
-    prep[3 * plane + p] = sp.sqt[p];
-    prep[4 * plane + p] = (float)(sp.box[p] * rk2 - (double)pb);
-    prep[5 * plane + p] = to_f(proj[p]);
-}
-
-// ---- the remainder diagonal D of a window layout with D = 64 n (BwdPlan::rem) ----
-// Its voxels (h, w, D) are the last element of every 1028-byte volume row; one strided pass
-// reads them (L2-line granular, ~1/32 of their lines is used, but they are 1/(D+1) of the
-// volume) instead of a fifth chunk of full sweeps with 1 live lane in 64.  Same arithmetic
-// as k_bwd_coop (fp32 A and V, shifted images).  Its terms go to compact arrays that
-// k_bwd_gather adds to the chunks' partial sums (so the three kernels depend on nothing but
-// k_bwd_prep and run beside k_bwd_coop on a second stream):
-//   remT[0..3][h][w] = A mp'(h, w+D), V Y(h, w+D), A mc'(h, w), V X(h, w)   (camera Am, B; projector Ac, Bp
-//   at o = w + D; gather's m' B products then include them)
-//   remT1[0][y][x] = p'(y, x+D) BoxA_D(y, x),  remT1[1][y][x+D] = c'(y, x) BoxA_D(y, x)   (T1c, T1p)
-// (2-D grids: blockIdx.y = the row, x = the column -- no 64-bit division per thread)
-__global__ __launch_bounds__(256) void k_bwd_rem_voxel(Geo g, BwdArgs a, float* remT, float* remA) {
-    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x, hv = blockIdx.y;
-    if (w >= g.WO) return;
-    const int64_t t = hv * g.WO + w, h = g.h_lo + hv, D = g.D;
-    const int64_t plane = g.H * g.W, pc = h * g.W + w, po = pc + D;
-    const int64_t e = t * g.DO + D;
-    const float X = a.Xc[pc], Y = a.Yp[po];
-    const float rS = __builtin_amdgcn_rsqf(__builtin_fmaf(X, Y, kEps));
-    const float A = a.grad[e] * rS;
-    const float V = A * a.vol[e] * rS;
-    remA[t] = A;
-    const int64_t n = g.HV() * g.WO;
-    remT[t] = A * a.mpp[po];
-    remT[n + t] = V * Y;
-    remT[2 * n + t] = A * a.mcc[pc];
-    remT[3 * n + t] = V * X;
-    (void)plane;
-}
-// vertical box of A_D: VA[y - ylo][w] = sum over volume rows h in [y - r, y + r]
-__global__ __launch_bounds__(256) void k_bwd_rem_vbox(Geo g, BwdArgs a, const float* remA, double* remV) {
-    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (w >= g.WO) return;
-    const int64_t t = (int64_t)blockIdx.y * g.WO + w, y = a.ylo + blockIdx.y;
-    int64_t h0 = y - g.r, h1 = y + g.r;
-    h0 = h0 > g.h_lo ? h0 : g.h_lo;
-    h1 = h1 < g.h_hi - 1 ? h1 : g.h_hi - 1;
-    double v = 0.0;
-    for (int64_t h = h0; h <= h1; ++h) v += (double)remA[(h - g.h_lo) * g.WO + w];
-    remV[t] = v;
-}
-// horizontal box and the T1 terms, camera column x in [-r, W) (x < 0: zero padding, c' = -cbar)
-__global__ __launch_bounds__(256) void k_bwd_rem_t1(Geo g, BwdArgs a, const double* remV, double* remT1) {
-    const int64_t xi = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (xi >= g.W + g.r) return;
-    const int64_t yy = blockIdx.y, x = xi - g.r, y = a.ylo + yy, D = g.D;
-    int64_t w0 = x - g.r, w1 = x + g.r;
-    w0 = w0 > 0 ? w0 : 0;
-    w1 = w1 < g.WO - 1 ? w1 : g.WO - 1;
-    double box = 0.0;
-    for (int64_t w = w0; w <= w1; ++w) box += remV[yy * g.WO + w];
-    const int64_t nyw = (a.yhi - a.ylo) * g.W;
-    const float cb = a.shift[0], pb = a.shift[1];
-    if (x >= 0) {  // camera pixel (y, x): p'(y, x + D), zero padded past the right edge
-        const float pv = x + D < g.W ? a.pp[y * g.W + x + D] : 0.f;
-        remT1[yy * g.W + x] = (double)(pv - pb) * box;
-    }
-    if (x + D >= 0 && x + D < g.W) {  // projector pixel (y, x + D); o < D - r gets no term (gather checks)
-        const float cv = x >= 0 ? a.cc[y * g.W + x] : 0.f;
-        remT1[nyw + yy * g.W + x + D] = (double)(cv - cb) * box;
-    }
-}
+// fp32 images for the sweep (after the shifts are known; written by the statistics pass,
+// stats.hip STATS_BWD_PREP): X = camera centred moment, mc' = camera patch mean - cbar,
+// c = camera; Y, mp', p likewise for the projector.  The images stay unshifted so that a
+// zero-padded (out-of-image) load minus the shift gives the shifted padding value -cbar / -pbar.
 
 constexpr int kSumBlocks = 512;
 
@@ -901,7 +1068,7 @@ struct BwdPlan {
     int nChunk, S, Sj, nRG, jc, nsegMax;
     bool ok;
     int64_t dlo, ylo, yhi;
-    bool rem;  // window, D = 64 n: diagonal D handled by k_bwd_rem_* (not a chunk)
+    bool rem;  // window, D = 64 n: diagonal D handled by remainder units (bwd_rem_body), not a chunk
     size_t part_bytes, acc_bytes, cover_bytes, prep_bytes, misc_bytes, rem_bytes;
 };
 
@@ -933,6 +1100,17 @@ bool cover_fits(const Geo& g, int64_t dlo, int nChunk, int S, int Sj) {
     return true;
 }
 
+// The window form's in-range offsets must stay below kWinNR: the gradient / volume rows one unit
+// reads (+ one row of columns and diagonals), and the six prepared images.
+bool win_path_ok(const Geo& g) {
+#ifdef CUSTMA_BWD_NOWIN
+    return false;
+#endif
+    const double slab = (double)g.WO * (double)g.DO * 4.0;
+    return g.layout == CUSTMA_LAYOUT_WINDOW && slab * (TRB + 2 * g.r + 2) < (double)kWinNR &&
+           (double)g.H * (double)g.W * 24.0 < (double)kWinNR;
+}
+
 BwdPlan plan_bwd(const Geo& g) {
     BwdPlan p;
     const int r = g.r;
@@ -942,9 +1120,9 @@ BwdPlan plan_bwd(const Geo& g) {
         p.nChunk = (int)cdiv((int64_t)g.D + 1, NLB);
         p.jc = 0;
         // D = 64 n: the last diagonal alone would take a fifth chunk of sweeps with one live lane
-        // in 64; k_bwd_rem_* add it instead (one strided pass over it, after k_bwd_gather)
+        // in 64; light units take it instead (bwd_rem_body, the window form only)
         const char* er = getenv("CUSTMA_BWD_NOREM");  // benchmarking only
-        if (g.D >= NLB && (g.D + 1) % NLB == 1 && !(er && atoi(er) != 0)) {
+        if (g.D >= NLB && (g.D + 1) % NLB == 1 && win_path_ok(g) && !(er && atoi(er) != 0)) {
             p.rem = true;
             p.nChunk -= 1;
         }
@@ -997,50 +1175,17 @@ BwdPlan plan_bwd(const Geo& g) {
     p.nRG = (int)cdiv(p.yhi - p.ylo, TRB);
     const size_t plane = (size_t)g.H * g.W;
     p.part_bytes = (size_t)NTYPE * p.S * plane * sizeof(float);
-    p.acc_bytes = 6 * plane * sizeof(double);
+    p.acc_bytes = 6 * plane * sizeof(acc_t);
     p.cover_bytes = 3 * (size_t)g.W * sizeof(int) + 3 * (size_t)g.W * p.S * sizeof(unsigned short);
     p.prep_bytes = 6 * plane * sizeof(float);
     p.misc_bytes = 2 * kSumBlocks * sizeof(double) + 256;
     // A of diagonal D [HV][WO] (fp32) and its vertical box [yhi - ylo][WO] (fp64)
     // remA [HV][WO] f32, its vertical box [yhi - ylo][WO] f64, remT [4][HV][WO] f32, remT1 [2][yhi - ylo][W] f64
-    p.rem_bytes = p.rem ? a256((size_t)g.HV() * g.WO * 4) + a256((size_t)(p.yhi - p.ylo) * g.WO * 8) +
-                              a256((size_t)4 * g.HV() * g.WO * 4) + (size_t)2 * (p.yhi - p.ylo) * g.W * 8
-                        : 0;
+    // remT [4][HV][WO] f32, remT1 [2][yhi - ylo][W] f32 (BwdArgs)
+    p.rem_bytes = p.rem ? a256((size_t)4 * g.HV() * g.WO * 4) + (size_t)2 * (p.yhi - p.ylo) * g.W * 4 : 0;
     return p;
 }
 
-
-// A second stream (and its fork / join events) per host thread and device, for work that may
-// overlap the sweep; created on first use, kept for the thread's life.
-struct SideStream {
-    hipStream_t st = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-hipError_t side_stream(SideStream** out) {
-    constexpr int kMaxDev = 64;
-    thread_local SideStream tab[kMaxDev];
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
-    SideStream& ss = tab[dev];
-    if (!ss.st) {
-        // CUSTMA_BWD_REM_PRIO=1: the side stream at the device's lowest priority, so the sweep's
-        // workgroups are dispatched first and the side kernels fill its tail (benchmarking)
-        int prio = 0;
-        const char* ep = getenv("CUSTMA_BWD_REM_PRIO");
-        if (ep && atoi(ep) == 1) {
-            int least = 0, greatest = 0;
-            if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return e;
-            prio = least;
-        }
-        if ((e = hipStreamCreateWithPriority(&ss.st, hipStreamNonBlocking, prio)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return e;
-    }
-    *out = &ss;
-    return hipSuccess;
-}
 
 template <typename T>
 hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp,
@@ -1049,7 +1194,7 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     char* w = (char*)ws;
     float* part = (float*)w;
     w += a256(p.part_bytes);
-    double* acc = (double*)w;
+    acc_t* acc = (acc_t*)w;
     w += a256(p.acc_bytes);
     int* cover = (int*)w;
     w += a256(p.cover_bytes);
@@ -1058,14 +1203,17 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     double* bsum = (double*)w;
     float* shift = (float*)(bsum + 2 * kSumBlocks);
     const int64_t n = g.H * g.W;
-    hipLaunchKernelGGL(k_img_blocksum<T>, dim3(kSumBlocks), dim3(256), 0, s, cam, n, bsum);
-    hipLaunchKernelGGL(k_img_blocksum<T>, dim3(kSumBlocks), dim3(256), 0, s, proj, n, bsum + kSumBlocks);
+    hipLaunchKernelGGL(k_img_blocksum<T>, dim3(kSumBlocks, 2), dim3(256), 0, s, cam, proj, n, bsum);
     hipLaunchKernelGGL(k_img_shift, dim3(1), dim3(256), 0, s, bsum, kSumBlocks, n, shift);
     hipLaunchKernelGGL(k_bwd_cover, dim3((unsigned)cdiv(g.W, 256)), dim3(256), 0, s, g, p.dlo, p.nChunk, p.S, p.Sj,
                        cover);
-    hipLaunchKernelGGL(k_bwd_prep<T>, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, g, cam, proj, sc, sp, shift, prep);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    // the patch sums (box, fp64, for k_bwd_combine2) and the six prepared fp32 images in one pass
+    // (stats.hip STATS_BWD_PREP; was box + sqt, then a separate k_bwd_prep pass over them)
+    if ((e = launch_stats(cam, proj, std::is_same<T, __half>::value ? CUSTMA_F16 : CUSTMA_F32, g, sc, sp, s,
+                          STATS_BWD_PREP, prep, shift)) != hipSuccess)
+        return e;
     BwdArgs a;
     a.cam = cam; a.proj = proj; a.sc = sc; a.sp = sp;
     a.grad = grad; a.vol = vol; a.shift = shift; a.part = part; a.cover = cover;
@@ -1074,43 +1222,29 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     a.dlo = p.dlo; a.ylo = p.ylo; a.yhi = p.yhi;
     a.order = g.layout == CUSTMA_LAYOUT_WINDOW ? 2 : 1;
     if (const char* eo = getenv("CUSTMA_BWD_ORDER")) a.order = atoi(eo);  // benchmarking only
-    // The remainder diagonal's kernels need only k_bwd_prep: they run on a second stream beside
-    // k_bwd_coop (their strided, latency-bound reads overlap the sweep) and k_bwd_gather waits
-    // for both.  CUSTMA_BWD_REM_SIDE=0 keeps them on the caller's stream (benchmarking only).
-    float* remT = nullptr;
-    double* remT1 = nullptr;
-    SideStream* side = nullptr;
+    a.remT = nullptr;
+    a.remT1 = nullptr;
     if (p.rem) {
         char* rw = (char*)bsum + a256(p.misc_bytes);  // the plan's rem_bytes follow misc_bytes
-        const size_t nA = a256((size_t)g.HV() * g.WO * 4), nV = a256((size_t)(p.yhi - p.ylo) * g.WO * 8);
-        float* remA = (float*)rw;
-        double* remV = (double*)(rw + nA);
-        remT = (float*)(rw + nA + nV);
-        remT1 = (double*)(rw + nA + nV + a256((size_t)4 * g.HV() * g.WO * 4));
-        hipStream_t rs = s;
-        const char* es = getenv("CUSTMA_BWD_REM_SIDE");
-        if (!(es && atoi(es) == 0)) {
-            if ((e = side_stream(&side)) != hipSuccess) return e;
-            if ((e = hipEventRecord(side->fork, s)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(side->st, side->fork, 0)) != hipSuccess) return e;
-            rs = side->st;
-        }
-        hipLaunchKernelGGL(k_bwd_rem_voxel, dim3((unsigned)cdiv(g.WO, 256), (unsigned)g.HV()), dim3(256), 0, rs, g, a,
-                           remT, remA);
-        hipLaunchKernelGGL(k_bwd_rem_vbox, dim3((unsigned)cdiv(g.WO, 256), (unsigned)(p.yhi - p.ylo)), dim3(256), 0, rs,
-                           g, a, remA, remV);
-        hipLaunchKernelGGL(k_bwd_rem_t1, dim3((unsigned)cdiv(g.W + g.r, 256), (unsigned)(p.yhi - p.ylo)), dim3(256), 0,
-                           rs, g, a, remV, remT1);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (side && (e = hipEventRecord(side->join, side->st)) != hipSuccess) return e;
+        a.remT = (float*)rw;
+        a.remT1 = (float*)(rw + a256((size_t)4 * g.HV() * g.WO * 4));
     }
-    const int64_t units = (int64_t)p.nChunk * p.nsegMax * p.nRG;
-    const unsigned blocks = (unsigned)(8 * (int64_t)p.nChunk * p.nsegMax * cdiv(p.nRG, 8));
+    const int nU = p.nChunk + (p.rem ? 1 : 0);  // chunk ranks of units (+ the remainder diagonal's)
+    const int64_t units = (int64_t)nU * p.nsegMax * p.nRG;
+    const unsigned blocks = (unsigned)(8 * (int64_t)nU * p.nsegMax * cdiv(p.nRG, 8));
     if (units > 0) {
+        const bool win = win_path_ok(g);
         prof_begin(PROF_BWD, s);
         switch (g.k) {
 #define CUSTMA_K(KK)                                                                              \
-    case KK: hipLaunchKernelGGL((k_bwd_coop<KK>), dim3(blocks), dim3(64 * NWC), 0, s, g, a); break;
+    case KK:                                                                                             \
+        if (win && p.rem)                                                                                \
+            hipLaunchKernelGGL((k_bwd_coop<KK, true, true>), dim3(blocks), dim3(64 * NWC), 0, s, g, a);  \
+        else if (win)                                                                                    \
+            hipLaunchKernelGGL((k_bwd_coop<KK, true, false>), dim3(blocks), dim3(64 * NWC), 0, s, g, a); \
+        else                                                                                             \
+            hipLaunchKernelGGL((k_bwd_coop<KK, false, false>), dim3(blocks), dim3(64 * NWC), 0, s, g, a); \
+        break;
             CUSTMA_SWEEP_KS(CUSTMA_K)
 #undef CUSTMA_K
             default: return hipErrorInvalidValue;
@@ -1118,14 +1252,13 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
         prof_end(PROF_BWD, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (side && (e = hipStreamWaitEvent(s, side->join, 0)) != hipSuccess) return e;
     // (gather and combine fused into one tiled pass -- the slot sums recomputed for each tile's r
     // halo -- measured slower: C5 backward op 29.5 -> 31.1 ms, C2 full 3.82 -> 3.95 ms)
     const int L = 16 + 2 * g.r;
     const size_t lds = sizeof(double) * 3 * (L * L + L * 16);
     const dim3 tiles((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2);
     hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2), dim3(256), 0, s, g, a, acc,
-                       remT, remT1);
+                       a.remT, a.remT1);
     hipLaunchKernelGGL(k_bwd_combine2<T>, tiles, dim3(256), lds, s, g, cam, proj, shift, acc, sc, sp, dcam, dproj);
     return hipGetLastError();
 }

@@ -84,9 +84,9 @@ void carve_stats(const Geo& g, void* ws, Stats* sc, Stats* sp) {
 }
 
 int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, void* ws, Stats* sc, Stats* sp,
-              hipStream_t s, bool box_only = false) {
+              hipStream_t s, int mode = STATS_FULL) {
     carve_stats(g, ws, sc, sp);
-    return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s, box_only), "stats");
+    return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s, mode), "stats");
 }
 
 int check_dtype(int32_t dtype) {
@@ -223,8 +223,10 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     if (workspace_bytes < stats_bytes(g)) return fail(CUSTMA_E_WORKSPACE, "workspace too small");
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
-    if (precision == CUSTMA_FAST && fast_supported(g.k))
+    const bool fast = precision == CUSTMA_FAST && fast_supported(g.k);
+    // the fast sweeps read sq and box only; the exact forward reads mean and sq
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, fast ? STATS_FWD : STATS_FULL))) return rc;
+    if (fast)
         return check_hip(launch_fwd_fast(camera, projector, dtype, g, sc, sp, cost_volume, s), "forward(fast)");
     return check_hip(launch_fwd_exact(camera, projector, dtype, g, sc, sp, cost_volume, s), "forward(exact)");
 }
@@ -259,9 +261,14 @@ int custma_backward_band(const float* grad, const float* cost_volume, const void
     const size_t need = stats_bytes(g) + align256(bwd_bytes(g)) + (cost_volume ? 0 : align256(volume_bytes(g)));
     if (workspace_bytes < need) return fail(CUSTMA_E_WORKSPACE, "workspace too small (%zu < %zu)", workspace_bytes, need);
     Stats sc, sp;
-    // with the forward's volume given, the backward reads only box and sqt (bwd_fused.hip,
-    // bwd_generic.hip): the two k^2-long fp32 chains of mean / sq are skipped
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, cost_volume != nullptr))) return rc;
+    // Statistics: a recompute needs the forward's (sq, box for the fast sweep; mean, sq for the exact
+    // one); given the forward's volume, the generic backward reads box and sqt, and the fused one
+    // computes its own (box + prepared images, one pass inside launch_backward) -- the k^2-long fp32
+    // chains of mean / sq are skipped either way
+    if (!cost_volume) rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, fused ? STATS_FWD : STATS_FULL);
+    else if (!fused) rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, STATS_BOX);
+    else carve_stats(g, workspace, &sc, &sp);
+    if (rc) return rc;
     char* ws2 = (char*)workspace + stats_bytes(g);
     if (!cost_volume) {  // recompute the forward into the workspace
         float* vol = (float*)(ws2 + align256(bwd_bytes(g)));

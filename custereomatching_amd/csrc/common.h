@@ -180,6 +180,18 @@ __device__ __forceinline__ void asm_ld4(uint32_t& a0, uint32_t& a1, uint32_t& a2
                   : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
                   : "v"(oA), "v"(oB), "v"(oC), "v"(oD), "s"(r0), "s"(r1), "s"(r2));
 }
+// Four loads through one descriptor, the first three at soffset sA, the fourth at sB.
+template <bool NOP = true>
+__device__ __forceinline__ void asm_ld4s(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t oA,
+                                         uint32_t oB, uint32_t oC, uint32_t oD, i32x4 r, uint32_t sA, uint32_t sB) {
+    CUSTMA_LD_ASM(NOP,
+                  "buffer_load_dword %0, %4, %8, %9 offen\n\t"
+                  "buffer_load_dword %1, %5, %8, %9 offen\n\t"
+                  "buffer_load_dword %2, %6, %8, %9 offen\n\t"
+                  "buffer_load_dword %3, %7, %8, %10 offen",
+                  : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+                  : "v"(oA), "v"(oB), "v"(oC), "v"(oD), "s"(r), "s"(sA), "s"(sB));
+}
 // Image-row groups for the forward sweep: 8 image loads (projector enter/leave x 2 halves,
 // camera enter/leave x 2 halves) / 6 statistics loads, rows selected by SGPR soffsets.
 // `s_nop 4` first: the soffsets may have been written by a VALU op (hazard note above).
@@ -299,9 +311,12 @@ inline hipError_t allow_lds(F* kernel, size_t bytes) {
 namespace custma {
 hipError_t launch_u8_to_unit(const uint8_t* src, int64_t npix, int C, int ch, int out_dtype, void* out,
                              hipStream_t s);
-// box_only: only box and sqt (what the backward reads); mean and sq are left unwritten
+// Which statistics launch_stats writes (stats.hip k_stats): FULL = mean, sq, box, sqt; BOX = box, sqt (the
+// generic backward); BWD_PREP = box + the fused backward's prepared images (`prep`, needs `shift`); FWD = sq,
+// box (what the fast forward sweeps read).
+enum StatsMode { STATS_FULL = 0, STATS_BOX = 1, STATS_BWD_PREP = 2, STATS_FWD = 3 };
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
-                        bool box_only = false);
+                        int mode = STATS_FULL, float* prep = nullptr, const float* shift = nullptr);
 hipError_t launch_fwd_exact(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             float* out, hipStream_t s);
 hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,

@@ -35,6 +35,13 @@ VARIANTS = {
     "ko_nomem_bar": (["CUSTMA_ABL_BWD_NOMEM", "CUSTMA_ABL_KO_BAR"], BWD),
     "ko_all": (["CUSTMA_ABL_BWD_NOMEM", "CUSTMA_ABL_KO_BAR", "CUSTMA_ABL_KO_RED", "CUSTMA_ABL_KO_SLIDE"], BWD),
     "bdp2ab1": (["CUSTMA_BWD_DEPTH=2", "CUSTMA_BWD_ABUF=1", "CUSTMA_BWD_FBC=6"], BWD),
+    # backward segment width (columns per unit)
+    "seg128": (["CUSTMA_BWD_SEG=128"], BWD), "seg256": (["CUSTMA_BWD_SEG=256"], BWD),
+    # backward without the window layout's SGPR-offset load path
+    "nowin": (["CUSTMA_BWD_NOWIN"], BWD),
+    "fbc8": (["CUSTMA_BWD_FBC=8"], BWD),
+    "acc64": (["CUSTMA_BWD_ACC64"], BWD),
+    "wait0vseq": (["CUSTMA_BWD_WAIT0", "CUSTMA_BWD_VSEQ"], BWD),  # round-3 step waits / vertical sum before  # fp64 per-pixel sums between gather and combine
 }
 for n in (sys.argv[1:] or VARIANTS):
     d, only = VARIANTS[n]
