@@ -119,7 +119,7 @@ def build_variant(libdir: str, defines, only=None) -> str:
     another directory; load it with CUSTMA_LIB=<path>.  `only`: the translation units the
     switches affect (the rest link from the main build's objects)."""
     os.makedirs(libdir, exist_ok=True)
-    extra = [f"-D{d}" for d in defines]
+    extra = [d if d.startswith("-") else f"-D{d}" for d in defines]  # "-f..." flags pass through
     todo = [u for u in UNITS if only is None or u[1] in only]
     if only is not None:
         build()

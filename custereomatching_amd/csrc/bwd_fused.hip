@@ -62,8 +62,11 @@ constexpr int NTYPE = 6;  // partial types: T1c, Am, B (camera) | T1p, Ac, Bp (p
 #ifndef CUSTMA_BWD_SEG
 #define CUSTMA_BWD_SEG 512  // 128 -> 512: C5 window backward 28.9 -> 27.6-28.0 ms, C2 full 3.57 -> 3.38 ms (profiles/r03/seg_ab.txt)
 #endif
-// pixel columns per unit (>= 64 + 2 r: segments s and s+2 never overlap); a unit sweeps kSeg + 2 r
-// columns, so the 2 r halo steps are 2 r / kSeg of redundant work
+// most pixel columns per unit; a unit sweeps its segment + 2 r columns, so the 2 r halo steps are
+// 2 r / segment of redundant work.  A chunk's columns are cut into equal segments of at most kSeg
+// (chunk_geo; an unequal last segment left the last round of units half idle: C3 has 4 segments
+// of 451 columns, not 3 of 512 + 1 of 266).  Every segment holds >= 64 + 2 r columns whenever a
+// chunk has two or more, so segments s and s + 2 never overlap (slot parity).
 constexpr int kSeg = CUSTMA_BWD_SEG;
 constexpr uint32_t kOOB = 0x80000000u;
 #ifndef CUSTMA_BWD_PF
@@ -79,9 +82,9 @@ __device__ __forceinline__ float ld_vol(__amdgpu_buffer_rsrc_t r, uint32_t off, 
 
 // Chunk geometry (host and device): diagonals [d0, d0+64); camera columns that carry
 // a valid voxel for some lane: [wlo, whi); pixel columns whose box touches one:
-// [wlo - r, whi + r), cut into segments of kSeg columns (one wave each).
+// [wlo - r, whi + r), cut into equal segments of seg <= kSeg columns (one unit each).
 struct ChunkGeo {
-    int64_t d0, wlo, whi;
+    int64_t d0, wlo, whi, seg;
 };
 __host__ __device__ inline ChunkGeo chunk_geo(const Geo& g, int64_t dlo, int j) {
     ChunkGeo c;
@@ -95,16 +98,18 @@ __host__ __device__ inline ChunkGeo chunk_geo(const Geo& g, int64_t dlo, int j) 
         const int64_t b = g.W - c.d0;
         c.whi = b < g.W ? b : g.W;
     }
+    const int64_t span = c.whi - c.wlo + 2 * (int64_t)g.r, n = span > kSeg ? (span + kSeg - 1) / kSeg : 1;
+    c.seg = span > 0 ? (span + n - 1) / n : 1;
     return c;
 }
 __host__ __device__ inline int chunk_nseg(const ChunkGeo& c, int r) {
-    return (int)((c.whi - c.wlo + 2 * r + kSeg - 1) / kSeg);
+    return (int)((c.whi - c.wlo + 2 * r + c.seg - 1) / c.seg);
 }
 // Segment s of chunk c: output pixel columns [xs, xe); the sweep runs w in [xs - r, xe + r).
 __host__ __device__ inline void seg_cols(const ChunkGeo& c, int r, int s, int64_t* xs, int64_t* xe) {
     const int64_t tlo = c.wlo - r, thi = c.whi + r;
-    *xs = tlo + (int64_t)s * kSeg;
-    const int64_t e = *xs + kSeg;
+    *xs = tlo + (int64_t)s * c.seg;
+    const int64_t e = *xs + c.seg;
     *xe = e < thi ? e : thi;
 }
 // Written column range [lo, hi) of partial type t for segment s of chunk c (before clipping
@@ -854,8 +859,12 @@ __host__ __device__ inline int cover_column(const Geo& g, int64_t dlo, int nChun
         const int ns = chunk_nseg(c, g.r);
         // the segment(s) of chunk j whose written range holds column x (<= 2, adjacent)
         const int64_t rel = x - (c.wlo - g.r) - (cls ? c.d0 : 0);
-        const int sa = (int)(rel >= 0 ? rel / kSeg : -((-rel + kSeg - 1) / kSeg));
-        for (int sg = sa - 1; sg <= sa + 1; ++sg) {
+        // segments whose written range can hold x: relative to segment s's own first column
+        // s seg, every range lies in [-2r - 1, seg + r + 63) (seg_range); checked exactly below
+        auto fdiv = [](int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
+        const int s_lo = (int)fdiv(rel - c.seg - g.r - NLB, c.seg);
+        const int s_hi = (int)fdiv(rel + 2 * g.r + 1, c.seg);
+        for (int sg = s_lo < 0 ? 0 : s_lo; sg <= s_hi; ++sg) {
             if (sg < 0 || sg >= ns) continue;
             seg_range(c, g.r, sg, t, &lo, &hi);
             if (x >= lo && x < hi) {
@@ -921,7 +930,8 @@ typedef double acc_t;
 typedef float acc_t;
 #endif
 
-// Sum the partial slots per pixel; out ([2 sides][3][H][W]): T1, Am|Ac, B|Bp (k_bwd_combine2
+// Sum the partial slots per pixel; out ([2 sides][3][H][W]): T1, Z = Am|Ac - m' B|Bp, B|Bp (k_bwd_combine3;
+// CUSTMA_BWD_GATHER1: T1, Am|Ac, B|Bp for k_bwd_combine2, the round-2 pair)
 // forms m' B as it loads its tile -- the same product, one fp64 array less through HBM).
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, acc_t* acc, const float* remT,
@@ -937,6 +947,12 @@ __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, acc_t* acc
 #pragma unroll
         for (int q = 0; q < 3; ++q) s[q] = gather_sum(g, a, remT, remT1, side, q, y, x, p);
     }
+#ifndef CUSTMA_BWD_GATHER1
+    // Z = A - m' B (m' = box / k^2 - shift, the pixel's shifted patch mean): k_bwd_combine3 then
+    // needs two box filters, Box[Z] = Box[A] - Box[m' B], and no patch sums
+    const double* box = side == 0 ? a.sc.box : a.sp.box;
+    s[1] -= s[2] * (box[p] / (double)(g.k * g.k) - (double)a.shift[side]);
+#endif
     acc_t* o = acc + (size_t)side * 3 * plane;
     o[p] = (acc_t)s[0];
     o[plane + p] = (acc_t)s[1];
@@ -1008,6 +1024,66 @@ __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict
     const int64_t q = y * g.W + x;
     const double ip = (double)to_f(img[q]) - (double)shift[side];
     out[q] = (float)((double)T1[q] - sa - ip * sb + sm);
+}
+
+// grad(y,x) = T1 - Box[Z] - img'(y,x) Box[B]   (k_bwd_gather2's Z = A - m' B; one side per blockIdx.z)
+// TS x TS output tiles (TS = 32: the (TS + 2r)^2 input halo is 1.7x the tile, 2.6x at 16); inputs
+// staged as fp32 (they are stored so), row sums and column sums in fp64, fixed order.
+template <typename T, int TS>
+__global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict__ cam, const T* __restrict__ proj,
+                                                      const float* __restrict__ shift, const acc_t* __restrict__ acc,
+                                                      float* __restrict__ dcam, float* __restrict__ dproj) {
+    extern __shared__ __attribute__((aligned(16))) double tl[];
+    const int side = blockIdx.z;
+    float* out = side == 0 ? dcam : dproj;
+    if (!out) return;
+    const T* img = side == 0 ? cam : proj;
+    const int64_t plane = g.H * g.W;
+    const acc_t* T1 = acc + (size_t)side * 3 * plane;
+    const acc_t* Zz = T1 + plane;
+    const acc_t* Bb = Zz + plane;
+    const int r = g.r, L = TS + 2 * r;
+    double* hZ = tl;                 // [L][TS] row sums
+    double* hB = hZ + L * TS;
+    float* tZ = (float*)(hB + L * TS);  // [L][L] inputs
+    float* tB = tZ + L * L;
+    const int64_t y0 = (int64_t)blockIdx.y * TS, x0 = (int64_t)blockIdx.x * TS;
+    const int Hi = (int)g.H, Wi = (int)g.W;
+    for (int e = threadIdx.x; e < L * L; e += 256) {
+        const int y = (int)y0 + e / L - r, x = (int)x0 + e % L - r;
+        const bool ok = y >= 0 && y < Hi && x >= 0 && x < Wi;
+        const int64_t q = (int64_t)y * Wi + x;
+        tZ[e] = ok ? (float)Zz[q] : 0.f;
+        tB[e] = ok ? (float)Bb[q] : 0.f;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < L * TS; e += 256) {
+        const int ry = e / TS, cx = e % TS;
+        double a = 0, b = 0;
+        for (int jx = 0; jx < g.k; ++jx) {
+            const int f = ry * L + cx + jx;
+            a += (double)tZ[f];
+            b += (double)tB[f];
+        }
+        hZ[e] = a;
+        hB[e] = b;
+    }
+    __syncthreads();
+    const double sh = (double)shift[side];
+    for (int e = threadIdx.x; e < TS * TS; e += 256) {
+        const int ly = e / TS, lx = e % TS;
+        const int64_t y = y0 + ly, x = x0 + lx;
+        if (y >= g.H || x >= g.W) continue;
+        double sz = 0, sb = 0;
+        for (int i = 0; i < g.k; ++i) {
+            const int f = (ly + i) * TS + lx;
+            sz += hZ[f];
+            sb += hB[f];
+        }
+        const int64_t q = y * g.W + x;
+        const double ip = (double)to_f(img[q]) - sh;
+        out[q] = (float)((double)T1[q] - sz - ip * sb);
+    }
 }
 
 // Image means (the global shifts cbar, pbar): per-block fp64 sums (blockIdx.y = the image; four
@@ -1259,7 +1335,18 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     const dim3 tiles((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2);
     hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2), dim3(256), 0, s, g, a, acc,
                        a.remT, a.remT1);
+#ifdef CUSTMA_BWD_GATHER1
     hipLaunchKernelGGL(k_bwd_combine2<T>, tiles, dim3(256), lds, s, g, cam, proj, shift, acc, sc, sp, dcam, dproj);
+#else
+    {
+        constexpr int TS3 = 32;
+        const int L3 = TS3 + 2 * g.r;
+        const size_t lds3 = sizeof(double) * 2 * L3 * TS3 + sizeof(float) * 2 * L3 * L3;
+        if ((e = allow_lds(k_bwd_combine3<T, TS3>, lds3)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_bwd_combine3<T, TS3>), dim3((unsigned)cdiv(g.W, TS3), (unsigned)cdiv(g.H, TS3), 2),
+                           dim3(256), lds3, s, g, cam, proj, shift, acc, dcam, dproj);
+    }
+#endif
     return hipGetLastError();
 }
 

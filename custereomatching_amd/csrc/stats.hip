@@ -11,8 +11,6 @@
 //   then k column taps), 2k fp64 adds per pixel instead of k^2.
 // sqt: fp64-accurate centred second moment box2 - box^2 / k^2 (separable too), rounded
 //   to fp32; only the backward reads it.
-#include <stdlib.h>
-
 #include <type_traits>
 
 #include "common.h"
@@ -21,7 +19,14 @@
 namespace custma {
 
 namespace {
-constexpr int TX = 16, TY = 64, PR = 4;  // 16 x 64 pixels per 256-thread workgroup, 4 rows per thread
+#ifndef CUSTMA_STATS_TX
+#define CUSTMA_STATS_TX 16
+#endif
+#ifndef CUSTMA_STATS_PR
+#define CUSTMA_STATS_PR 4
+#endif
+// TX x TY pixels per 256-thread workgroup, PR rows per thread (a tap row read from LDS feeds PR pixels)
+constexpr int TX = CUSTMA_STATS_TX, PR = CUSTMA_STATS_PR, TY = 256 / TX * PR;
 static_assert(PR % 2 == 0, "pixel pairs");
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -205,137 +210,6 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
         }
     }
 }
-// Compile-time k (the sweep sizes): one thread = one image column x 16 consecutive rows, a
-// workgroup = 64 columns x 64 rows (four waves of 16-row strips), so every store instruction
-// writes one 64-column row segment (256 B fp32 / 512 B fp64) and a tap row read from LDS feeds
-// every pixel of the strip whose patch holds it (up to k chains in flight per thread, packed in
-// pixel pairs where both hold the row).  The fp64 patch sums accumulate the k-tap row sums per
-// pixel (exact, like the separable form).  The k^2-long fp32 chains keep the reference's (i, j)
-// order per pixel, so mean and sq are bit-identical to k_stats.  The tap-row loop is not unrolled
-// (fully unrolled, the compiler keeps every row's values live: > 256 VGPRs); the pixel loops are,
-// with wave-uniform branches on which pixels hold the row.
-constexpr int S2X = 64, S2Y = 64, S2P = 16;  // tile columns, tile rows, rows per thread
-template <typename T, int K, int MODE>
-__global__ __launch_bounds__(256) void k_stats2(const T* __restrict__ img0, const T* __restrict__ img1, Geo g,
-                                                Stats st0, Stats st1, float* __restrict__ prep,
-                                                const float* __restrict__ shift) {
-    constexpr int R = K / 2, LX = S2X + 2 * R, LY = S2Y + 2 * R, NR = S2P + K - 1;  // tap rows per strip
-    constexpr bool CHAINS = MODE == STATS_FULL || MODE == STATS_FWD;         // mean / sq
-    constexpr bool SQT = MODE == STATS_FULL || MODE == STATS_BOX || MODE == STATS_BWD_PREP;
-    const T* __restrict__ img = blockIdx.z ? img1 : img0;
-    const Stats st = blockIdx.z ? st1 : st0;
-    __shared__ float tile[LY][LX];
-    const int x0 = blockIdx.x * S2X, y0 = blockIdx.y * S2Y;
-    const int Hi = (int)g.H, Wi = (int)g.W;
-    for (int e = threadIdx.x; e < LY * LX; e += 256) {
-        const int ty = e / LX, tx = e % LX;
-        const int y = y0 + ty - R, x = x0 + tx - R;
-        tile[ty][tx] = (y >= 0 && y < Hi && x >= 0 && x < Wi) ? to_f(img[(int64_t)y * Wi + x]) : 0.f;
-    }
-    __syncthreads();
-    const int lx = threadIdx.x & 63, ys = (threadIdx.x >> 6) * S2P;  // column, first row of the strip
-    const float* trow = &tile[ys][lx];
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    float m[S2P], q[S2P];
-    double bx[S2P], bx2[S2P];
-#pragma unroll
-    for (int p = 0; p < S2P; ++p) { m[p] = 0.f; q[p] = 0.f; bx[p] = 0.0; bx2[p] = 0.0; }
-    // pass 1: patch sums and the mean chains; tap row i2 is row i2 - p of pixel p's patch,
-    // p in [i2 - K + 1, i2]
-#pragma unroll 1
-    for (int i2 = 0; i2 < NR; ++i2) {
-        float v[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) v[j] = trow[i2 * LX + j];
-        double a = 0.0, b = 0.0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            a += (double)v[j];
-            if constexpr (SQT) b = fma((double)v[j], (double)v[j], b);
-        }
-#pragma unroll
-        for (int p = 0; p < S2P; p += 2) {
-            const bool in0 = p >= i2 - K + 1 && p <= i2, in1 = p + 1 >= i2 - K + 1 && p + 1 <= i2;
-            if (in0) { bx[p] += a; if constexpr (SQT) bx2[p] += b; }
-            if (in1) { bx[p + 1] += a; if constexpr (SQT) bx2[p + 1] += b; }
-            if constexpr (CHAINS) {
-                if (in0 && in1) {  // both pixels hold the row: packed (the same IEEE op per half)
-                    f32x2 acc = {m[p], m[p + 1]};
-#pragma unroll
-                    for (int j = 0; j < K; ++j) acc = acc + f32x2{v[j], v[j]};
-                    m[p] = acc.x;
-                    m[p + 1] = acc.y;
-                } else if (in0) {
-#pragma unroll
-                    for (int j = 0; j < K; ++j) m[p] = m[p] + v[j];
-                } else if (in1) {
-#pragma unroll
-                    for (int j = 0; j < K; ++j) m[p + 1] = m[p + 1] + v[j];
-                }
-            }
-        }
-    }
-    if constexpr (CHAINS) {
-#pragma unroll
-        for (int p = 0; p < S2P; ++p) m[p] = m[p] / (float)(K * K);
-        // pass 2: the centred-square chains, same row order
-#pragma unroll 1
-        for (int i2 = 0; i2 < NR; ++i2) {
-            float v[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j) v[j] = trow[i2 * LX + j];
-#pragma unroll
-            for (int p = 0; p < S2P; p += 2) {
-                const bool in0 = p >= i2 - K + 1 && p <= i2, in1 = p + 1 >= i2 - K + 1 && p + 1 <= i2;
-                if (in0 && in1) {
-                    const f32x2 mm = {m[p], m[p + 1]};
-                    f32x2 acc = {q[p], q[p + 1]};
-#pragma unroll
-                    for (int j = 0; j < K; ++j) {
-                        const f32x2 c = f32x2{v[j], v[j]} - mm;
-                        acc = __builtin_elementwise_fma(c, c, acc);
-                    }
-                    q[p] = acc.x;
-                    q[p + 1] = acc.y;
-                } else if (in0 || in1) {
-                    const int pp = in0 ? p : p + 1;
-                    float qq = in0 ? q[p] : q[p + 1];
-                    const float mp = in0 ? m[p] : m[p + 1];
-#pragma unroll
-                    for (int j = 0; j < K; ++j) {
-                        const float c = v[j] - mp;
-                        qq = __builtin_fmaf(c, c, qq);
-                    }
-                    if (pp == p) q[p] = qq; else q[p + 1] = qq;
-                }
-            }
-        }
-    }
-    const int x = x0 + lx;
-    if (x >= Wi) return;
-    const int64_t n = g.H * g.W;
-#pragma unroll
-    for (int p = 0; p < S2P; ++p) {
-        const int y = y0 + ys + p;
-        if (y >= Hi) break;
-        const int64_t o = (int64_t)y * Wi + x;
-        if constexpr (MODE == STATS_FULL) st.mean[o] = m[p];
-        if constexpr (CHAINS) st.sq[o] = q[p];
-        st.box[o] = bx[p];
-        if constexpr (SQT) {
-            const double c2 = bx2[p] - bx[p] * bx[p] / (double)(K * K);
-            const float sqt = (float)(c2 > 0.0 ? c2 : 0.0);
-            if constexpr (MODE == STATS_BWD_PREP) {
-                float* pz = prep + 3 * n * blockIdx.z;
-                pz[o] = sqt;
-                pz[n + o] = (float)(bx[p] / (double)(K * K) - (double)shift[blockIdx.z]);
-                pz[2 * n + o] = trow[(p + R) * LX + R];  // raw: the sweep subtracts the shift after a zero-padded load
-            } else {
-                st.sqt[o] = sqt;
-            }
-        }
-    }
-}
 }  // namespace
 
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
@@ -344,21 +218,11 @@ hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo&
     const int LX = TX + 2 * g.r, LY = TY + 2 * g.r;
     const size_t lds = sizeof(double) * 2 * LY * TX + sizeof(float) * LY * LX;
     hipError_t err = hipSuccess;
-    const char* e2 = getenv("CUSTMA_STATS1");  // benchmarking only: the 16 x 64 tile kernel for every k
-    const bool v2 = !(e2 && atoi(e2) != 0);
-    const dim3 grid2((unsigned)cdiv(g.W, S2X), (unsigned)cdiv(g.H, S2Y), 2);
     auto go = [&](auto kc) {
         constexpr int KT = decltype(kc)::value;
         auto launch = [&](auto* cast, auto mc) {
             using T = std::remove_const_t<std::remove_pointer_t<decltype(cast)>>;
             constexpr int M = decltype(mc)::value;
-            if constexpr (KT > 0) {
-                if (v2) {
-                    hipLaunchKernelGGL((k_stats2<T, KT, M>), grid2, dim3(256), 0, s, (const T*)cam, (const T*)proj, g,
-                                       sc, sp, prep, shift);
-                    return;
-                }
-            }
             if ((err = allow_lds(k_stats<T, KT, M>, lds)) != hipSuccess) return;
             hipLaunchKernelGGL((k_stats<T, KT, M>), grid, dim3(256), lds, s, (const T*)cam, (const T*)proj, g, sc, sp,
                                prep, shift);

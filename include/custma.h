@@ -11,8 +11,10 @@
  * contiguous, of element type `dtype`.  Outputs are written fully (no
  * pre-zeroing needed).  `workspace` is device memory of at least
  * custma_workspace_bytes(...) bytes, owned by the caller (the torch caching
- * allocator in the Python shim); nothing is allocated inside a call, so
- * every call is hipGraph-capturable.
+ * allocator in the Python shim); nothing is allocated inside a call, no
+ * internal stream or event is used and nothing synchronises, so every call is
+ * hipGraph-capturable (tests/test_gpu_graph.py captures forward + backward
+ * into a torch.cuda.CUDAGraph and replays it bit-identically).
  */
 #ifndef CUSTMA_H
 #define CUSTMA_H

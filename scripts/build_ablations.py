@@ -16,7 +16,7 @@ VARIANTS = {
     "nostore": (["CUSTMA_ABL_NOSTORE"], FWD), "noupdate": (["CUSTMA_ABL_NOUPDATE"], FWD),
     "storeonly": (["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT"], FWD),
     "nowait": (["CUSTMA_ABL_NOWAIT"], FWD), "stats7": (["CUSTMA_ABL_STATS7"], FWD),
-    "early": (["CUSTMA_TILE_EARLY"], FWD),
+    "early": (["CUSTMA_TILE_EARLY"], FWD), "tileP3": (["CUSTMA_TILE_P=3"], FWD),
     # volume-store cache policy (gfx950 aux bits: 1 sc0, 2 nt, 16 sc1)
     "st_plain": (["CUSTMA_STORE_AUX=0"], FWD), "st_sc1": (["CUSTMA_STORE_AUX=16"], FWD),
     "st_ntsc1": (["CUSTMA_STORE_AUX=18"], FWD),
@@ -41,7 +41,11 @@ VARIANTS = {
     "nowin": (["CUSTMA_BWD_NOWIN"], BWD),
     "fbc8": (["CUSTMA_BWD_FBC=8"], BWD),
     "acc64": (["CUSTMA_BWD_ACC64"], BWD),
-    "wait0vseq": (["CUSTMA_BWD_WAIT0", "CUSTMA_BWD_VSEQ"], BWD),  # round-3 step waits / vertical sum before  # fp64 per-pixel sums between gather and combine
+    "wait0vseq": (["CUSTMA_BWD_WAIT0", "CUSTMA_BWD_VSEQ"], BWD),
+    "noslp": (["-fno-slp-vectorize"], BWD + ["stats.hip"]),  # no packed-fp32 pairing by the compiler
+    "gather1": (["CUSTMA_BWD_GATHER1"], BWD),
+    # statistics tile: 16 x 64 pixels, 4 rows per thread is the default (32 x 8: C5 0.80 -> 0.98 ms)
+    "stats32x8": (["CUSTMA_STATS_TX=32", "CUSTMA_STATS_PR=8"], ["stats.hip"]),  # the per-pixel slot gather + 16x16 three-map combine  # round-3 step waits / vertical sum before  # fp64 per-pixel sums between gather and combine
 }
 for n in (sys.argv[1:] or VARIANTS):
     d, only = VARIANTS[n]
