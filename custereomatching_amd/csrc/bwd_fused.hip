@@ -697,28 +697,35 @@ __device__ __forceinline__ void bwd_rem_body(const Geo& g, const BwdArgs& a, int
     const uint32_t vMc = own ? img_row_a(kMc) : kWinNR, vC = own ? img_row_a(kC) : kWinNR;
     const uint32_t vMp = own && img_row_a(kMp) != kWinNR ? img_row_a(kMp) + (uint32_t)Di * 4u : kWinNR;
     const uint32_t vP = own ? img_row_a(kP) : kWinNR;
-    const auto rG = make_rsrc(a.grad + (size_t)(vrow0 - g.h_lo) * slab, kWinNR);
-    const auto rV = make_rsrc(a.vol + (size_t)(vrow0 - g.h_lo) * slab, kWinNR);
-    const auto rP = make_rsrc(a.Xc, kWinNR);
+    // Loads as inline asm issued RP - 1 steps ahead with hand-counted waits: compiler-visible loads
+    // were waited for before each barrier (the compiler drains them there), so every step of a
+    // remainder unit paid a whole memory latency (C5: the units cost 4.2 ms of k_bwd_coop's 25.0).
+    const i32x4 dG = make_rsrc_sgpr(a.grad + (size_t)(vrow0 - g.h_lo) * slab, kWinNR);
+    const i32x4 dV = make_rsrc_sgpr(a.vol + (size_t)(vrow0 - g.h_lo) * slab, kWinNR);
+    const i32x4 dP = make_rsrc_sgpr(a.Xc, kWinNR);
     const uint32_t gsU4 = (uint32_t)g.DO * 4u;
-    struct Ld { float g, v, x, y, mp, mc, c, p; };
-    auto load = [&](int w, Ld& b) {
+    struct Ld { uint32_t g, v, x, y, mp, mc, c, p; };
+    auto issue = [&](int w, Ld& b) {
         const int xb = w - R, xd = xb + Di;
         const bool wv_ok = w >= 0 && w < WOi;  // volume column (and projector column w + D < W)
-        const uint32_t sW = wv_ok ? (uint32_t)w * gsU4 : kWinNR;
-        const uint32_t sC = (w >= 0 && w < Wi) ? (uint32_t)w * 4u : kWinNR;
-        const uint32_t sCD = wv_ok ? (uint32_t)w * 4u : kWinNR;
-        const uint32_t sX = (xb >= 0 && xb < Wi) ? (uint32_t)xb * 4u : kWinNR;
-        const uint32_t sXD = (xd >= 0 && xd < Wi) ? (uint32_t)xd * 4u : kWinNR;
-        b.g = ld_bufs<float>(rG, vG, sW);
-        b.v = ld_bufs<float>(rV, vG, sW);
-        b.x = ld_bufs<float>(rP, vX, sC);
-        b.y = ld_bufs<float>(rP, vY, sCD);
-        b.mp = ld_bufs<float>(rP, vMp, sCD);
-        b.mc = ld_bufs<float>(rP, vMc, sC);
-        b.c = ld_bufs<float>(rP, vC, sX);
-        b.p = ld_bufs<float>(rP, vP, sXD);
+        // SGPR soffsets (readfirstlane: never an illegal literal operand, never a VGPR copy)
+        const uint32_t sW = __builtin_amdgcn_readfirstlane(wv_ok ? (uint32_t)w * gsU4 : kWinNR);
+        const uint32_t sC = __builtin_amdgcn_readfirstlane((w >= 0 && w < Wi) ? (uint32_t)w * 4u : kWinNR);
+        const uint32_t sCD = __builtin_amdgcn_readfirstlane(wv_ok ? (uint32_t)w * 4u : kWinNR);
+        const uint32_t sX = __builtin_amdgcn_readfirstlane((xb >= 0 && xb < Wi) ? (uint32_t)xb * 4u : kWinNR);
+        const uint32_t sXD = __builtin_amdgcn_readfirstlane((xd >= 0 && xd < Wi) ? (uint32_t)xd * 4u : kWinNR);
+        asm_ld2s(b.g, b.v, vG, vG, dG, dV, sW, sW);
+        asm_ld2s(b.x, b.mc, vX, vMc, dP, dP, sC, sC);
+        asm_ld2s(b.y, b.mp, vY, vMp, dP, dP, sCD, sCD);
+        asm_ld2s(b.c, b.p, vC, vP, dP, dP, sX, sXD);
     };
+    auto tie = [&](Ld& b) {
+        asm_tie(b.g); asm_tie(b.v); asm_tie(b.x); asm_tie(b.mc);
+        asm_tie(b.y); asm_tie(b.mp); asm_tie(b.c); asm_tie(b.p);
+    };
+    auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
+    constexpr int RP = 4, NLR = 8, NSR = 6;  // load buffers; loads per step; stores per flush
+    static_assert(FBC % RP == 0, "flush blocks start on load buffer 0");
     const int64_t nvR = g.HV() * g.WO, nywR = (a.yhi - a.ylo) * g.W;
     const auto rT = make_rsrc(a.remT, (uint32_t)(4 * nvR * 4));
     const auto rT1 = make_rsrc(a.remT1, (uint32_t)(2 * nywR * 4));
@@ -727,41 +734,56 @@ __device__ __forceinline__ void bwd_rem_body(const Geo& g, const BwdArgs& a, int
         for (int s2 = 0; s2 < K; ++s2) ringD[s2 * TRW + lane] = 0.f;
     float HVD = 0.f;
     int sidx = 0;
-    Ld cur, nxt;
-    load(w0, cur);
+    auto step = [&](Ld& cur, Ld& nxt, int w, int s, bool flushed) {
+        // cur was issued RP - 1 steps ago; after it: the next RP - 2 steps' loads and, for the first
+        // RP - 1 steps of a block after a flush, that flush's stores
+        if (flushed && s < RP - 1) asm_vmcnt<(RP - 2) * NLR + NSR>();
+        else asm_vmcnt<(RP - 2) * NLR>();
+        tie(cur);
+        issue(w + RP - 1, nxt);  // past the segment's end: in range or masked, never used
+        const float rSD = __builtin_amdgcn_rsqf(__builtin_fmaf(F(cur.x), F(cur.y), kEps));
+        const float AD = F(cur.g) * rSD;
+        float* AbD = AbufD + ((w - w0) & 1) * NY;
+        if (row >= 0) AbD[row] = AD;
+        const float VD = AD * F(cur.v) * rSD;
+        const float rsvD = ringD[sidx * TRW + (lane & (TRW - 1))];
+        __syncthreads();  // the unit's A_D of this step is published (double-buffered)
+        const float xD = lane < TRW + 2 * R ? AbD[yw + lane] : 0.f;
+        float vD = xD;  // lane m: unit rows yw + m .. yw + m + 2R (lanes m .. m + 2R)
+        if constexpr (TRW - 1 + 2 * R < 16) {
+            Unroll<1, 2 * R + 1>::run([&](auto ic) { vD += dpp<0x100 + decltype(ic)::value>(xD); });  // row_shl
+        } else {
+#pragma unroll
+            for (int i = 1; i <= 2 * R; ++i) vD += AbD[yw + (lane & (TRW - 1)) + i];
+        }
+        HVD += vD - rsvD;
+        if (own) {
+            ringD[sidx * TRW + lane] = vD;
+            float* rb = remb[s][lane];
+            rb[0] = AD * F(cur.mp);            // camera Am at (row, w):  A mp'(row, w + D)
+            rb[1] = VD * F(cur.y);             // camera B  at (row, w):  V Y(row, w + D)
+            rb[2] = AD * F(cur.mc);            // projector Ac at (row, w + D): A mc'(row, w)
+            rb[3] = VD * F(cur.x);             // projector Bp at (row, w + D): V X(row, w)
+            rb[4] = (F(cur.p) - pb) * HVD;     // T1c at (row, xb): p'(row, xb + D) BoxA_D
+            rb[5] = (F(cur.c) - cb) * HVD;     // T1p at (row, xb + D): c'(row, xb) BoxA_D
+        }
+        sidx = sidx + 1 == K ? 0 : sidx + 1;
+    };
+    Ld L[RP];
+    issue(w0, L[0]);
+    issue(w0 + 1, L[1]);
+    issue(w0 + 2, L[2]);
     for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
         const int nsteps = min(FBC, wend - wfirst);
-        for (int s = 0; s < nsteps; ++s) {
-            const int w = wfirst + s;
-            load(w + 1, nxt);  // past the segment's end: in range or masked, never used
-            const float rSD = __builtin_amdgcn_rsqf(__builtin_fmaf(cur.x, cur.y, kEps));
-            const float AD = cur.g * rSD;
-            float* AbD = AbufD + ((w - w0) & 1) * NY;
-            if (row >= 0) AbD[row] = AD;
-            const float VD = AD * cur.v * rSD;
-            const float rsvD = ringD[sidx * TRW + (lane & (TRW - 1))];
-            __syncthreads();  // the unit's A_D of this step is published (double-buffered)
-            const float xD = lane < TRW + 2 * R ? AbD[yw + lane] : 0.f;
-            float vD = xD;  // lane m: unit rows yw + m .. yw + m + 2R (lanes m .. m + 2R)
-            if constexpr (TRW - 1 + 2 * R < 16) {
-                Unroll<1, 2 * R + 1>::run([&](auto ic) { vD += dpp<0x100 + decltype(ic)::value>(xD); });  // row_shl
-            } else {
-#pragma unroll
-                for (int i = 1; i <= 2 * R; ++i) vD += AbD[yw + (lane & (TRW - 1)) + i];
-            }
-            HVD += vD - rsvD;
-            if (own) {
-                ringD[sidx * TRW + lane] = vD;
-                float* rb = remb[s][lane];
-                rb[0] = AD * cur.mp;               // camera Am at (row, w):  A mp'(row, w + D)
-                rb[1] = VD * cur.y;                // camera B  at (row, w):  V Y(row, w + D)
-                rb[2] = AD * cur.mc;               // projector Ac at (row, w + D): A mc'(row, w)
-                rb[3] = VD * cur.x;                // projector Bp at (row, w + D): V X(row, w)
-                rb[4] = (cur.p - pb) * HVD;        // T1c at (row, xb): p'(row, xb + D) BoxA_D
-                rb[5] = (cur.c - cb) * HVD;        // T1p at (row, xb + D): c'(row, xb) BoxA_D
-            }
-            sidx = sidx + 1 == K ? 0 : sidx + 1;
-            cur = nxt;
+        const bool fl = wfirst > w0;
+        for (int s = 0; s < nsteps; s += RP) {
+            step(L[0], L[3], wfirst + s, s, fl);
+            if (s + 1 >= nsteps) break;
+            step(L[1], L[0], wfirst + s + 1, s + 1, fl);
+            if (s + 2 >= nsteps) break;
+            step(L[2], L[1], wfirst + s + 2, s + 2, fl);
+            if (s + 3 >= nsteps) break;
+            step(L[3], L[2], wfirst + s + 3, s + 3, fl);
         }
         // flush: lane (jcol, m) stores the six terms of step wfirst + jcol, own row m
         int ln = lane;
@@ -780,6 +802,10 @@ __device__ __forceinline__ void bwd_rem_body(const Geo& g, const BwdArgs& a, int
         const int o = x + Di;
         st_buf(rv[5], rT1, (xok && o >= 0 && o < Wi) ? (uint32_t)(nywR * 4) + ty + (uint32_t)(o * 4) : kOOB);
     }
+    // the last steps' prefetches are still in flight: keep their registers live until they have landed
+    asm_vmcnt<0>();
+#pragma unroll
+    for (int i = 0; i < RP; ++i) tie(L[i]);
 }
 
 #ifdef CUSTMA_BWD_WPE
