@@ -12,6 +12,9 @@ CFGS = {
     "c3_win": dict(H=2048, W=2048, k=11, D=256, layout="window", dtype=torch.float16),
     "c3_full": dict(H=2048, W=2048, k=11, D=256, layout="full", dtype=torch.float16),
     "c5_win": dict(H=4096, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
+    # kernel sizes without a sweep instantiation (exact forward + generic fp64 backward)
+    "c3_win_k17": dict(H=2048, W=2048, k=17, D=256, layout="window", dtype=torch.float16),
+    "c3_win_k16": dict(H=2048, W=2048, k=16, D=256, layout="window", dtype=torch.float16),
 }
 
 def run(name, ops, reps):

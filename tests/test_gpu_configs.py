@@ -139,6 +139,29 @@ def test_config2_forward_backward_full_size(gpu, layout, D):
         assert _rel(p.grad[h0:h1].cpu().numpy(), rp) <= 1e-5
 
 
+# ---------------- generic fp64 backward (even k, odd k > 15) at a mid size ----------------
+
+@pytest.mark.parametrize("layout,D,k", [("window", 64, 16), ("full", 0, 17)])
+def test_generic_backward_mid_size(gpu, layout, D, k):
+    """Mid-size problems through the banded generic backward (grid-stride kernels, bounded workspace;
+    the 512 x 512 full layout takes two bands of output rows at the default 2 GiB band budget),
+    checked on haloed oracle bands."""
+    H = W = 1024 if layout == "window" else 512
+    o = k // 2
+    cam, proj = make_pair(H, W, max(D, 1), seed=85)
+    c, p = _dev(cam, gpu), _dev(proj, gpu)
+    vol = cm.cost_volume_forward(c, p, D, k, layout, "exact")
+    gen = torch.Generator(device=gpu).manual_seed(86)
+    g = torch.randn(vol.shape, generator=gen, device=gpu)
+    gc, gp = cm.cost_volume_backward(g, c, p, k, layout, D, projector_grad=True, cost_volume=vol)
+    for h0 in (0, H // 2 + 3, H - 3):
+        h1 = min(H, h0 + 3)
+        a0, a1 = max(0, h0 - 2 * o), min(H, h1 + 2 * o)
+        rc, rp = _band_backward(g[a0:a1].cpu().numpy(), cam, proj, k, h0, h1, layout, D)
+        assert _rel(gc[h0:h1].cpu().numpy(), rc) <= 1e-5
+        assert _rel(gp[h0:h1].cpu().numpy(), rp) <= 1e-5
+
+
 # ---------------- configs[3]: 2048x2048 fp16, D=256, k=11, window ----------------
 
 def test_config3_window_fp16(gpu):

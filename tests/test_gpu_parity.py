@@ -248,6 +248,23 @@ def test_backward_both_images(gpu, case, layout):
     assert np.abs(gp - rp).max() <= tol_p, np.abs(gp - rp).max() / max(1.0, np.abs(rp).max())
 
 
+@pytest.mark.parametrize("case", [(20, 44, 17, 9, "textured"), (18, 36, 4, 10, "smooth")], ids=["k17", "k4"])
+@pytest.mark.parametrize("layout", [FULL, WIN])
+def test_backward_generic_small_bands(gpu, case, layout, monkeypatch):
+    """The generic fp64 backward's band loop (A / VA / BA recomputed per band of output rows, halo
+    included) with 3-row bands gives the same gradients as the oracle."""
+    monkeypatch.setenv("CUSTMA_GEN_BAND_ROWS", "3")
+    H, W, k, D, kind = case
+    cam, proj = make_pair(H, W, max(D, 1), seed=33, kind=kind)
+    lay, Dl = _layout_args(layout, D)
+    g = _rand_grad(O.volume_shape(H, W, lay, Dl), 8)
+    rc, rp = O.backward_f64(g, cam, proj, k, layout=lay, D=Dl)
+    gc, gp = cm.cost_volume_backward(_dev(g, gpu), _dev(cam, gpu), _dev(proj, gpu), k, layout, D,
+                                     camera_grad=True, projector_grad=True)
+    assert np.abs(gc.cpu().numpy() - rc).max() <= 1e-5 * max(1.0, np.abs(rc).max())
+    assert np.abs(gp.cpu().numpy() - rp).max() <= 1e-5 * max(1.0, np.abs(rp).max())
+
+
 def test_backward_ones_matches_reference_golden(gpu):
     """g = ones, exactly what examples/verify.py:68,123 backpropagates."""
     import glob
