@@ -1,7 +1,7 @@
 // Backward for every kernel size the fused sweep (bwd_fused.hip) has no
 // instantiation for: even k (taps at offsets -k/2 .. k-1-k/2, the reference's
 // `kernel_size / 2` origin, custma/src/stereo_matching_kernel.cu:103-105, 172-173)
-// and odd k > 15.  Same decomposition as the fused path, every sum in fp64:
+// and odd k > 17.  Same decomposition as the fused path, every sum in fp64:
 //
 //   dC(y,x) = T1c(y,x) - sum_box [Am + c(y,x) B - mc B]
 //   dP(y,o) = T1p(y,o) - sum_box [Ac + p(y,o) Bp - mp Bp]

@@ -55,7 +55,7 @@ extern "C" {
 #define CUSTMA_E_LAUNCH (-4)    /* HIP launch / runtime error */
 #define CUSTMA_E_UNSUPPORTED (-5)
 
-/* kernel_size range.  Odd k <= 15 run the sliding-window (fast) kernels; every other size -- odd k up to
+/* kernel_size range.  Odd k <= 17 run the sliding-window (fast) kernels; every other size -- odd k up to
  * CUSTMA_MAX_KERNEL and even k, whose taps sit at offsets -k/2 .. k-1-k/2 exactly as the reference's
  * `kernel_size / 2` origin (stereo_matching_kernel.cu:44,60) -- runs the exact forward and the generic
  * fp64 backward. */

@@ -72,9 +72,9 @@ def test_entry_points_validate_before_launch():
     assert L.custma_forward(None, None, 0, 8, 8, 5, 1, 8, 1, None, None, 0, None) == _lib.E_ARG  # D >= W
     assert L.custma_forward(None, None, 0, 8, 8, 5, 0, 0, 1, None, None, 0, None) == _lib.E_NULL
     assert L.custma_forward(None, None, 0, 0, 8, 5, 0, 0, 1, None, None, 0, None) == 0  # empty image: no-op
-    # k = 17 has no fused instantiation: the generic backward takes it, validating first
+    # k = 19 has no fused instantiation: the generic backward takes it, validating first
     fake = 4096  # never dereferenced: the null gradient is rejected before any launch
-    assert L.custma_backward(None, None, None, None, 0, 8, 8, 17, 0, 0, fake, None, None, 0, None) == _lib.E_NULL
+    assert L.custma_backward(None, None, None, None, 0, 8, 8, 19, 0, 0, fake, None, None, 0, None) == _lib.E_NULL
     assert L.custma_argmax(None, 4, 0, None, None, None) == _lib.E_ARG
     assert L.custma_disparity(None, None, 0, 8, 8, 5, 0, 0, None, None, None, None, 0, None) == _lib.E_NULL
 

@@ -48,6 +48,7 @@ CASES = [
     (24, 48, 7, 0, "textured"),
     (26, 40, 5, 39, "textured"),
     (19, 37, 21, 9, "textured"),  # beyond the sweep instantiations: exact kernel only
+    (30, 70, 17, 31, "textured"),  # the largest sweep instantiation (16 + 2r = 32 columns)
     (20, 44, 4, 9, "textured"),   # even k: taps at -k/2 .. k/2-1 (reference .cu:44,60), exact kernel
     (17, 33, 10, 6, "smooth"),
     (12, 70, 33, 20, "textured"),  # above the old limit of 31
@@ -81,7 +82,7 @@ def test_fast_forward_within_bound(gpu, case, layout):
     assert got.shape == ref.shape
     assert np.abs(got - ref).max() <= O.fast_tolerance(k)
     truth = O.forward_f64(cam, proj, k, layout=lay, D=Dl)
-    # vs the fp64 truth: the reference's own worst-case rounding (k > 15 runs the exact
+    # vs the fp64 truth: the reference's own worst-case rounding (k > 17 runs the exact
     # reference arithmetic, whose k^2-long fp32 chain can exceed 1e-5 of the truth)
     assert np.abs(got - truth).max() <= O.cost_error_bound(k)
 
@@ -157,7 +158,8 @@ DISP_CASES = [
     (30, 64, 11, 16, "smooth"),
     (24, 48, 5, 16, "constant"),
     (24, 48, 5, 16, "zeros"),
-    (20, 40, 17, 12, "textured"),  # no sweep instance: every pixel decided exactly
+    (20, 40, 19, 12, "textured"),  # no sweep instance: every pixel decided exactly
+    (24, 64, 17, 20, "textured"),  # the largest sweep instance
     (20, 40, 4, 12, "textured"),   # even k, likewise
 ]
 
@@ -221,8 +223,11 @@ BWD_CASES = [
     (20, 100, 5, 64, "textured"),
     (18, 300, 11, 256, "smooth"),
     (16, 140, 15, 128, "quantized"),
-    # generic fp64 backward (no fused instantiation): odd k > 15 and even k
-    (20, 44, 17, 9, "textured"),
+    # k = 17: the largest fused instantiation (one workgroup per CU: 92 KB of LDS)
+    (26, 80, 17, 20, "textured"),
+    (20, 140, 17, 64, "smooth"),
+    # generic fp64 backward (no fused instantiation): odd k > 17 and even k
+    (20, 44, 19, 9, "textured"),
     (16, 40, 25, 12, "smooth"),
     (18, 36, 4, 10, "textured"),
     (15, 30, 6, 8, "quantized"),
@@ -248,7 +253,7 @@ def test_backward_both_images(gpu, case, layout):
     assert np.abs(gp - rp).max() <= tol_p, np.abs(gp - rp).max() / max(1.0, np.abs(rp).max())
 
 
-@pytest.mark.parametrize("case", [(20, 44, 17, 9, "textured"), (18, 36, 4, 10, "smooth")], ids=["k17", "k4"])
+@pytest.mark.parametrize("case", [(20, 44, 19, 9, "textured"), (18, 36, 4, 10, "smooth")], ids=["k19", "k4"])
 @pytest.mark.parametrize("layout", [FULL, WIN])
 def test_backward_generic_small_bands(gpu, case, layout, monkeypatch):
     """The generic fp64 backward's band loop (A / VA / BA recomputed per band of output rows, halo
@@ -450,7 +455,7 @@ def _soft_argmax_ref(vol, beta):
 
 SOFT_CASES = [
     (24, 96, 5, 24, "full"), (24, 96, 9, 40, "window"), (20, 320, 11, 256, "window"),  # tile kernel
-    (18, 200, 7, 150, "window"), (20, 40, 17, 12, "full"), (16, 48, 4, 10, "window"),  # exact-decided
+    (18, 200, 7, 150, "window"), (20, 40, 19, 12, "full"), (16, 48, 4, 10, "window"),  # exact-decided
     (24, 48, 5, 16, "full"),
 ]
 
