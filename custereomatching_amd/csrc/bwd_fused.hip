@@ -145,7 +145,7 @@ struct BwdArgs {
     const float* shift;  // [2]: cbar, pbar
     float* part;         // [NTYPE][S][H][W]
     // window layouts with D = 64 n (BwdPlan::rem): the remainder diagonal D's terms, written by the
-    // remainder units (bwd_rem_body), added by k_bwd_gather:
+    // row-walking remainder kernel (k_bwd_rem_rows), added by k_bwd_gather:
     //   remT [4][HV][WO]       A mp'(h, w+D), V Y(h, w+D), A mc'(h, w), V X(h, w)
     //   remT1[2][yhi-ylo][W]   T1c at (y, x): p'(y, x+D) BoxA_D(y, x);  T1p at (y, x+D): c'(y, x) BoxA_D(y, x)
     float* remT;
@@ -646,166 +646,115 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 }
 
 // The remainder diagonal D of a window with D = 64 n (BwdPlan::rem): its voxels (h, w, D) are the
-// float right after the last chunk's 64 in every volume row.  They run as an extra chunk rank of
-// units (k_bwd_coop, j == nChunk) dispatched with the full chunks of the same (row group, segment),
-// so their lines are the ones those units are reading (L2 hits; a separate pass reads one
-// 128-byte line per voxel).  A remainder unit is cheap: lanes 0..3 of wave v take its own rows
-// 4v .. 4v+3 and lanes 4.. its share of the halo rows; A_D goes to a small LDS row array (one
-// barrier per step), the own rows' vertical box is a DPP window sum over those lanes, the
-// horizontal box slides through a K-deep LDS ring, and the six terms of each own row go through
-// an LDS buffer to coalesced-per-row stores every FBC steps (a.remT / a.remT1, added by
-// k_bwd_gather).  Same fp32 arithmetic as the sweep.
+// float right after the last chunk's 64 in every volume row, so every one of them is a separate
+// 128-byte line.  They are not swept with the chunks: a fifth chunk of sweeps with one live lane
+// in 64, or light units whose lanes are unit rows (eight loads per step, each lane a different
+// line of the gradient, the volume and the six prepared images: 445 M line requests per C5 launch
+// beside the sweep's ~1 G), both cost k_bwd_coop ~4 ms at C5 (20.8 ms without the diagonal,
+// profiles/r03/rem).  k_bwd_rem_rows instead walks ROWS with lanes = 64 consecutive camera
+// columns w: per step (volume row h) two strided loads (gradient and volume at diagonal D: one
+// line per lane, unavoidable), the prepared-image values coalesced, A_D and V_D, the vertical box
+// of A_D as a K-deep sliding sum in registers (the row loop unrolled K times), the horizontal box
+// through a wave-private LDS row (no barrier), and the six terms stored per row (a.remT / a.remT1,
+// added by k_bwd_gather).  A wave owns the 64 - 2R middle columns of its 64 (the outer R on each
+// side only feed the horizontal box); one wave per (column tile, row band).  Same fp32 arithmetic
+// as the sweep's other diagonals.
+constexpr int kRemRB = 64;  // output rows per row band
+
 template <int K>
-__device__ __forceinline__ void bwd_rem_body(const Geo& g, const BwdArgs& a, int sg, int rg, float* AbufD,
-                                             float* ringD, float (*remb)[4][6]) {
-    constexpr int R = K / 2, NY = TRB + 2 * R, NH = 2 * R;
-    constexpr int FBC = fbc_for<K>();
-    constexpr int HPW = (NH + NWC - 1) / NWC;
-    static_assert(TRW + HPW <= 16, "the rows of a wave fit one 16-lane DPP row");
-    const ChunkGeo cg = chunk_geo(g, a.dlo, 0);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int Wi = (int)g.W, Hi = (int)g.H, WOi = (int)g.WO, Di = (int)g.D;
-    const int64_t y0 = a.ylo + (int64_t)TRB * rg;
-    const int y0i = (int)y0, ir0 = y0i - R;
-    int64_t xs64, xe64;
-    seg_cols(cg, R, sg, &xs64, &xe64);
-    const int xs = (int)xs64, xe = (int)xe64, w0 = xs - R, wend = xe + R;
-    const int yw = TRW * wv;
-    const int hlo = (int)g.h_lo, hhi = (int)g.h_hi;
+__global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntile) {
+    constexpr int R = K / 2, OWN = 64 - 2 * R;
+    __shared__ float xs_[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t unit = (int64_t)blockIdx.x * 4 + wv;
+    const int tile = (int)(unit % ntile);
+    const int64_t band = unit / ntile;
+    const int64_t y0 = a.ylo + band * kRemRB;
+    if (y0 >= a.yhi) return;
+    const int64_t y1 = min(a.yhi, y0 + kRemRB);
+    const int Wi = (int)g.W, WOi = (int)g.WO, Di = (int)g.D, hlo = (int)g.h_lo, hhi = (int)g.h_hi, Hi = (int)g.H;
+    const int x0 = -R + tile * OWN;          // first output column of this wave
+    const int w = x0 - R + lane;             // this lane's camera column (voxel column)
+    const bool own = lane >= R && lane < 64 - R;  // lane's column is one of this wave's outputs
+    const bool wok = w >= 0 && w < WOi;      // a voxel column of diagonal D
     const size_t slab = (size_t)g.WO * g.DO, plane = (size_t)g.H * g.W;
-    const int64_t vrow0 = max(g.h_lo, y0 - R);
-    const int vrow0i = (int)vrow0;
-    const uint32_t vstride = (uint32_t)(slab * 4), pb4 = (uint32_t)(plane * 4);
     const float cb = a.shift[0], pb = a.shift[1];
+    const uint32_t pb4 = (uint32_t)(plane * 4);
     enum { kX = 0, kMc = 1, kC = 2, kY = 3, kMp = 4, kP = 5 };
-    // this lane's row (unit row index) and its offsets (kWinNR: none / outside)
-    int row = -1;
-    if (lane < TRW) row = R + yw + lane;
-    else if (lane < TRW + HPW && wv + NWC * (lane - TRW) < NH) {
-        const int q = wv + NWC * (lane - TRW);
-        row = q < R ? q : q + TRB;
-    }
-    const int img = row >= 0 ? ir0 + row : -1;
-    auto img_row_a = [&](int arr) -> uint32_t {
-        return (row >= 0 && img >= 0 && img < Hi) ? (uint32_t)(img * Wi * 4) + arr * pb4 : kWinNR;
-    };
-    const bool own = lane < TRW;
-    const uint32_t vG = (row >= 0 && img >= hlo && img < hhi) ? (uint32_t)(img - vrow0i) * vstride + (uint32_t)Di * 4u
-                                                              : kWinNR;
-    const uint32_t vX = img_row_a(kX), vY = img_row_a(kY) == kWinNR ? kWinNR : img_row_a(kY) + (uint32_t)Di * 4u;
-    const uint32_t vMc = own ? img_row_a(kMc) : kWinNR, vC = own ? img_row_a(kC) : kWinNR;
-    const uint32_t vMp = own && img_row_a(kMp) != kWinNR ? img_row_a(kMp) + (uint32_t)Di * 4u : kWinNR;
-    const uint32_t vP = own ? img_row_a(kP) : kWinNR;
-    // Loads as inline asm issued RP - 1 steps ahead with hand-counted waits: compiler-visible loads
-    // were waited for before each barrier (the compiler drains them there), so every step of a
-    // remainder unit paid a whole memory latency (C5: the units cost 4.2 ms of k_bwd_coop's 25.0).
-    const i32x4 dG = make_rsrc_sgpr(a.grad + (size_t)(vrow0 - g.h_lo) * slab, kWinNR);
-    const i32x4 dV = make_rsrc_sgpr(a.vol + (size_t)(vrow0 - g.h_lo) * slab, kWinNR);
-    const i32x4 dP = make_rsrc_sgpr(a.Xc, kWinNR);
-    const uint32_t gsU4 = (uint32_t)g.DO * 4u;
-    struct Ld { uint32_t g, v, x, y, mp, mc, c, p; };
-    auto issue = [&](int w, Ld& b) {
-        const int xb = w - R, xd = xb + Di;
-        const bool wv_ok = w >= 0 && w < WOi;  // volume column (and projector column w + D < W)
-        // SGPR soffsets (readfirstlane: never an illegal literal operand, never a VGPR copy)
-        const uint32_t sW = __builtin_amdgcn_readfirstlane(wv_ok ? (uint32_t)w * gsU4 : kWinNR);
-        const uint32_t sC = __builtin_amdgcn_readfirstlane((w >= 0 && w < Wi) ? (uint32_t)w * 4u : kWinNR);
-        const uint32_t sCD = __builtin_amdgcn_readfirstlane(wv_ok ? (uint32_t)w * 4u : kWinNR);
-        const uint32_t sX = __builtin_amdgcn_readfirstlane((xb >= 0 && xb < Wi) ? (uint32_t)xb * 4u : kWinNR);
-        const uint32_t sXD = __builtin_amdgcn_readfirstlane((xd >= 0 && xd < Wi) ? (uint32_t)xd * 4u : kWinNR);
-        asm_ld2s(b.g, b.v, vG, vG, dG, dV, sW, sW);
-        asm_ld2s(b.x, b.mc, vX, vMc, dP, dP, sC, sC);
-        asm_ld2s(b.y, b.mp, vY, vMp, dP, dP, sCD, sCD);
-        asm_ld2s(b.c, b.p, vC, vP, dP, dP, sX, sXD);
-    };
-    auto tie = [&](Ld& b) {
-        asm_tie(b.g); asm_tie(b.v); asm_tie(b.x); asm_tie(b.mc);
-        asm_tie(b.y); asm_tie(b.mp); asm_tie(b.c); asm_tie(b.p);
-    };
-    auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
-    constexpr int RP = 4, NLR = 8, NSR = 6;  // load buffers; loads per step; stores per flush
-    static_assert(FBC % RP == 0, "flush blocks start on load buffer 0");
+    // volume rows of this band: [y0 - R, y1 + R) clipped to [h_lo, h_hi); offsets relative to vb
+    const int vb = (int)max((int64_t)hlo, y0 - R);
+    const auto rG = make_rsrc(a.grad + (size_t)(vb - hlo) * slab, 0x7FFFFFF0u);
+    const auto rV = make_rsrc(a.vol + (size_t)(vb - hlo) * slab, 0x7FFFFFF0u);
+    const auto rP = make_rsrc(a.Xc, 0x7FFFFFF0u);
+    constexpr uint32_t OOB = 0x80000000u;
+    const uint32_t vcol = wok ? (uint32_t)((size_t)w * g.DO + Di) * 4u : OOB;  // voxel (., w, D) in a row
+    const uint32_t vstride = (uint32_t)(slab * 4);
     const int64_t nvR = g.HV() * g.WO, nywR = (a.yhi - a.ylo) * g.W;
     const auto rT = make_rsrc(a.remT, (uint32_t)(4 * nvR * 4));
     const auto rT1 = make_rsrc(a.remT1, (uint32_t)(2 * nywR * 4));
-    if (own)
-#pragma unroll
-        for (int s2 = 0; s2 < K; ++s2) ringD[s2 * TRW + lane] = 0.f;
-    float HVD = 0.f;
-    int sidx = 0;
-    auto step = [&](Ld& cur, Ld& nxt, int w, int s, bool flushed) {
-        // cur was issued RP - 1 steps ago; after it: the next RP - 2 steps' loads and, for the first
-        // RP - 1 steps of a block after a flush, that flush's stores
-        if (flushed && s < RP - 1) asm_vmcnt<(RP - 2) * NLR + NSR>();
-        else asm_vmcnt<(RP - 2) * NLR>();
-        tie(cur);
-        issue(w + RP - 1, nxt);  // past the segment's end: in range or masked, never used
-        const float rSD = __builtin_amdgcn_rsqf(__builtin_fmaf(F(cur.x), F(cur.y), kEps));
-        const float AD = F(cur.g) * rSD;
-        float* AbD = AbufD + ((w - w0) & 1) * NY;
-        if (row >= 0) AbD[row] = AD;
-        const float VD = AD * F(cur.v) * rSD;
-        const float rsvD = ringD[sidx * TRW + (lane & (TRW - 1))];
-        __syncthreads();  // the unit's A_D of this step is published (double-buffered)
-        const float xD = lane < TRW + 2 * R ? AbD[yw + lane] : 0.f;
-        float vD = xD;  // lane m: unit rows yw + m .. yw + m + 2R (lanes m .. m + 2R)
-        if constexpr (TRW - 1 + 2 * R < 16) {
-            Unroll<1, 2 * R + 1>::run([&](auto ic) { vD += dpp<0x100 + decltype(ic)::value>(xD); });  // row_shl
-        } else {
-#pragma unroll
-            for (int i = 1; i <= 2 * R; ++i) vD += AbD[yw + (lane & (TRW - 1)) + i];
-        }
-        HVD += vD - rsvD;
-        if (own) {
-            ringD[sidx * TRW + lane] = vD;
-            float* rb = remb[s][lane];
-            rb[0] = AD * F(cur.mp);            // camera Am at (row, w):  A mp'(row, w + D)
-            rb[1] = VD * F(cur.y);             // camera B  at (row, w):  V Y(row, w + D)
-            rb[2] = AD * F(cur.mc);            // projector Ac at (row, w + D): A mc'(row, w)
-            rb[3] = VD * F(cur.x);             // projector Bp at (row, w + D): V X(row, w)
-            rb[4] = (F(cur.p) - pb) * HVD;     // T1c at (row, xb): p'(row, xb + D) BoxA_D
-            rb[5] = (F(cur.c) - cb) * HVD;     // T1p at (row, xb + D): c'(row, xb) BoxA_D
-        }
-        sidx = sidx + 1 == K ? 0 : sidx + 1;
+    float* xs = xs_[wv];
+    struct Ld { float g, v, x, y, mp, mc; };
+    // loads of volume row h (zero outside the volume rows / columns: A_D = 0 there)
+    auto load = [&](int h, Ld& b) {
+        const bool hv = h >= hlo && h < hhi, hi = h >= 0 && h < Hi;
+        const uint32_t vo = hv && vcol != OOB ? (uint32_t)(h - vb) * vstride + vcol : OOB;
+        const uint32_t io = hi ? (uint32_t)(h * Wi) * 4u : OOB;
+        b.g = ld_buf<float>(rG, vo);
+        b.v = ld_buf<float>(rV, own ? vo : OOB);
+        b.x = ld_buf<float>(rP, io != OOB && w >= 0 && w < Wi ? io + (uint32_t)w * 4u + kX * pb4 : OOB);
+        b.y = ld_buf<float>(rP, io != OOB && wok ? io + (uint32_t)(w + Di) * 4u + kY * pb4 : OOB);
+        b.mp = ld_buf<float>(rP, io != OOB && wok && own ? io + (uint32_t)(w + Di) * 4u + kMp * pb4 : OOB);
+        b.mc = ld_buf<float>(rP, io != OOB && wok && own ? io + (uint32_t)w * 4u + kMc * pb4 : OOB);
     };
-    Ld L[RP];
-    issue(w0, L[0]);
-    issue(w0 + 1, L[1]);
-    issue(w0 + 2, L[2]);
-    for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
-        const int nsteps = min(FBC, wend - wfirst);
-        const bool fl = wfirst > w0;
-        for (int s = 0; s < nsteps; s += RP) {
-            step(L[0], L[3], wfirst + s, s, fl);
-            if (s + 1 >= nsteps) break;
-            step(L[1], L[0], wfirst + s + 1, s + 1, fl);
-            if (s + 2 >= nsteps) break;
-            step(L[2], L[1], wfirst + s + 2, s + 2, fl);
-            if (s + 3 >= nsteps) break;
-            step(L[3], L[2], wfirst + s + 3, s + 3, fl);
-        }
-        // flush: lane (jcol, m) stores the six terms of step wfirst + jcol, own row m
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const int jcol = ln % FBC, m = (ln / FBC) & 3;
-        const bool live = jcol < nsteps && ln < 4 * FBC;
-        const int w = wfirst + jcol, x = w - R, y = y0i + yw + m;
-        const float* rv = remb[jcol][m];
-        const bool wok = live && w >= xs && w < xe && w >= 0 && w < WOi && y >= hlo && y < hhi;
-        const uint32_t tv = (uint32_t)(((y - hlo) * WOi + w) * 4), tn = (uint32_t)(nvR * 4);
+    float ring[K];  // A_D of the last K rows (slot = step mod K)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) st_buf(rv[t], rT, wok ? tv + t * tn : kOOB);
-        const bool xok = live && x >= xs && x < xe && y < (int)a.yhi;
-        const uint32_t ty = (uint32_t)((y - (int)a.ylo) * Wi * 4);
-        st_buf(rv[4], rT1, (xok && x >= 0 && x < Wi) ? ty + (uint32_t)(x * 4) : kOOB);
-        const int o = x + Di;
-        st_buf(rv[5], rT1, (xok && o >= 0 && o < Wi) ? (uint32_t)(nywR * 4) + ty + (uint32_t)(o * 4) : kOOB);
+    for (int i = 0; i < K; ++i) ring[i] = 0.f;
+    float VS = 0.f;  // vertical sum of A_D over rows h - K + 1 .. h
+    const int hs = (int)(y0 - R), he = (int)(y1 + R);  // rows walked; output y = h - R for y in [y0, y1)
+    Ld cur, nxt;
+    load(hs, cur);
+    for (int hb = hs; hb < he; hb += K) {
+        Unroll<0, K>::run([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const int h = hb + i;
+            if (h < he) {
+                load(h + 1, nxt);  // past the band: in range or masked, unused
+                const float rSD = __builtin_amdgcn_rsqf(__builtin_fmaf(cur.x, cur.y, kEps));
+                const float AD = cur.g * rSD, VD = AD * cur.v * rSD;
+                VS += AD - ring[i];
+                ring[i] = AD;
+                // per-voxel terms of (h, w): stored by the lanes that own column w
+                if (own && wok && h >= hlo && h < hhi && h >= y0 && h < y1) {  // each row by one band
+                    const uint32_t tv = (uint32_t)(((int64_t)(h - hlo) * WOi + w) * 4), tn = (uint32_t)(nvR * 4);
+                    st_buf(AD * cur.mp, rT, tv);           // camera Am at (h, w):  A mp'(h, w + D)
+                    st_buf(VD * cur.y, rT, tv + tn);       // camera B  at (h, w):  V Y(h, w + D)
+                    st_buf(AD * cur.mc, rT, tv + 2 * tn);  // projector Ac at (h, w + D): A mc'(h, w)
+                    st_buf(VD * cur.x, rT, tv + 3 * tn);   // projector Bp at (h, w + D): V X(h, w)
+                }
+                // output row y = h - R: BoxA_D(y, x) = sum of VS over the lanes x - R .. x + R
+                const int y = h - R;
+                if (y >= y0) {
+                    xs[lane] = VS;
+                    float c[2 * R + 1];
+#pragma unroll
+                    for (int j = 0; j <= 2 * R; ++j) c[j] = xs[own ? lane - R + j : 0];
+                    const float box = tree_sum<2 * R + 1>(c);
+                    const int x = w;  // output column of an own lane
+                    if (own) {
+                        const uint32_t ty = (uint32_t)((y - (int)a.ylo) * Wi * 4);
+                        const uint32_t yi = (uint32_t)(y * Wi) * 4u;
+                        // T1c at (y, x): p'(y, x + D) BoxA_D;  T1p at (y, x + D): c'(y, x) BoxA_D
+                        const int xd = x + Di;
+                        const float pv = ld_buf<float>(rP, xd >= 0 && xd < Wi ? yi + (uint32_t)xd * 4u + kP * pb4 : OOB);
+                        const float cv = ld_buf<float>(rP, x >= 0 && x < Wi ? yi + (uint32_t)x * 4u + kC * pb4 : OOB);
+                        if (x >= 0 && x < Wi) st_buf((pv - pb) * box, rT1, ty + (uint32_t)x * 4u);
+                        if (xd >= 0 && xd < Wi) st_buf((cv - cb) * box, rT1, (uint32_t)(nywR * 4) + ty + (uint32_t)xd * 4u);
+                    }
+                }
+                cur = nxt;
+            }
+        });
     }
-    // the last steps' prefetches are still in flight: keep their registers live until they have landed
-    asm_vmcnt<0>();
-#pragma unroll
-    for (int i = 0; i < RP; ++i) tie(L[i]);
 }
 
 #ifdef CUSTMA_BWD_WPE
@@ -813,7 +762,7 @@ __device__ __forceinline__ void bwd_rem_body(const Geo& g, const BwdArgs& a, int
 #else
 #define CUSTMA_BWD_OCC
 #endif
-template <int K, bool WIN, bool REM>
+template <int K, bool WIN>
 __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, BwdArgs a) {
     // XCD x owns row groups [x nRGx, (x+1) nRGx) (their halo rows are read on one XCD).
     // A wave's 256-byte gradient / volume row segment spans three 128-byte lines whose outer
@@ -824,10 +773,9 @@ __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, Bwd
     //   FETCH 140 -> 103 GB per launch, 37.1 -> 35.7 ms op).
     // a.order 1 (full layout, up to 2W/64 chunks of very different lengths): row group fastest,
     //   then chunk rank (longest first), then segment (C2 full: 4.36 -> 3.85-4.05 ms op).
-    // REM: one more chunk rank, j == nChunk: the remainder diagonal's units (bwd_rem_body)
     const int64_t hb = blockIdx.x, xi = hb / 8, x = hb % 8;
     const int nRGx = (a.nRG + 7) / 8;
-    const int nU = a.nChunk + (REM ? 1 : 0);
+    const int nU = a.nChunk;
     int j, sg, rg;
     if (a.order == 2) {
         const int jr = (int)(xi % nU);
@@ -835,17 +783,17 @@ __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, Bwd
         rg = (int)(x * nRGx + rest % nRGx);
         const int64_t sg64 = rest / nRGx;
         if (rg >= a.nRG || sg64 >= a.nsegMax) return;
-        j = REM && jr == a.nChunk ? jr : chunk_of_rank(jr, a.nChunk, a.jc);
+        j = chunk_of_rank(jr, a.nChunk, a.jc);
         sg = (int)sg64;
     } else {
         const int64_t unit = xi / nRGx;
         rg = (int)(x * nRGx + xi % nRGx);
         if (rg >= a.nRG || unit >= (int64_t)nU * a.nsegMax) return;
         const int jr = (int)(unit % nU);
-        j = REM && jr == a.nChunk ? jr : chunk_of_rank(jr, a.nChunk, a.jc);
+        j = chunk_of_rank(jr, a.nChunk, a.jc);
         sg = (int)(unit / nU);
     }
-    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, REM && j == a.nChunk ? 0 : j), g.r)) return;
+    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
     constexpr int NY = TRB + 2 * (K / 2);
     __shared__ __attribute__((aligned(16))) float Abuf[NAB * NY * 64];
     __shared__ __attribute__((aligned(16))) float ring[NWC * K * TRW * 64];
@@ -853,15 +801,6 @@ __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, Bwd
     __shared__ __attribute__((aligned(16))) float cbuf[NWC][FBC][12];
     __shared__ __attribute__((aligned(16))) float pbuf[NWC][FBC][12];
     const int wv = threadIdx.x >> 6;
-    if constexpr (REM) {
-        if (j == a.nChunk) {  // the remainder diagonal's unit: its small buffers alias the sweep's
-            float* AbufD = Abuf;                                         // [2][NY]
-            float* ringD = ring + 2 * NY + wv * (K * TRW);               // [NWC][K][TRW]
-            float(*remb)[4][6] = (float(*)[4][6])(ring + 2 * NY + NWC * K * TRW) + wv * FBC;  // [NWC][FBC][4][6]
-            bwd_rem_body<K>(g, a, sg, rg, AbufD, ringD, remb);
-            return;
-        }
-    }
     bwd_coop_body<K, WIN>(g, a, j, sg, rg, Abuf, ring + wv * (K * TRW * 64), cbuf[wv], pbuf[wv]);
 }
 
@@ -932,7 +871,7 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
     }
     if (i < n) v0 += (double)base[(size_t)sl[i] * plane];
     double s = v0 + v1;
-    if (remT) {  // the remainder diagonal's terms (bwd_rem_body)
+    if (remT) {  // the remainder diagonal's terms (k_bwd_rem_rows)
         const int64_t nyw = (a.yhi - a.ylo) * g.W, nv = g.HV() * g.WO, yy = y - a.ylo, D = g.D;
         if (q == 0) {
             // written for camera columns x < WO + r (past them the box of diagonal D is empty) and
@@ -1170,7 +1109,7 @@ struct BwdPlan {
     int nChunk, S, Sj, nRG, jc, nsegMax;
     bool ok;
     int64_t dlo, ylo, yhi;
-    bool rem;  // window, D = 64 n: diagonal D handled by remainder units (bwd_rem_body), not a chunk
+    bool rem;  // window, D = 64 n: diagonal D handled by k_bwd_rem_rows, not a chunk
     size_t part_bytes, acc_bytes, cover_bytes, prep_bytes, misc_bytes, rem_bytes;
 };
 
@@ -1222,7 +1161,7 @@ BwdPlan plan_bwd(const Geo& g) {
         p.nChunk = (int)cdiv((int64_t)g.D + 1, NLB);
         p.jc = 0;
         // D = 64 n: the last diagonal alone would take a fifth chunk of sweeps with one live lane
-        // in 64; light units take it instead (bwd_rem_body, the window form only)
+        // in 64; k_bwd_rem_rows takes it instead (the window form only)
         const char* er = getenv("CUSTMA_BWD_NOREM");  // benchmarking only
         if (g.D >= NLB && (g.D + 1) % NLB == 1 && win_path_ok(g) && !(er && atoi(er) != 0)) {
             p.rem = true;
@@ -1331,27 +1270,40 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
         a.remT = (float*)rw;
         a.remT1 = (float*)(rw + a256((size_t)4 * g.HV() * g.WO * 4));
     }
-    const int nU = p.nChunk + (p.rem ? 1 : 0);  // chunk ranks of units (+ the remainder diagonal's)
+    const int nU = p.nChunk;  // chunk ranks of units (p.rem: diagonal D by k_bwd_rem_rows)
     const int64_t units = (int64_t)nU * p.nsegMax * p.nRG;
     const unsigned blocks = (unsigned)(8 * (int64_t)nU * p.nsegMax * cdiv(p.nRG, 8));
+    // k_bwd_rem_rows: one wave per (column tile of 64 - 2r owned columns over [-r, WO + r), row band)
+    const int rem_tiles = (int)cdiv(g.WO + 2 * g.r, 64 - 2 * g.r);
+    const int64_t rem_units = (int64_t)rem_tiles * cdiv(p.yhi - p.ylo, kRemRB);
     if (units > 0) {
         const bool win = win_path_ok(g);
         prof_begin(PROF_BWD, s);
         switch (g.k) {
 #define CUSTMA_K(KK)                                                                              \
     case KK:                                                                                             \
-        if (win && p.rem)                                                                                \
-            hipLaunchKernelGGL((k_bwd_coop<KK, true, true>), dim3(blocks), dim3(64 * NWC), 0, s, g, a);  \
-        else if (win)                                                                                    \
-            hipLaunchKernelGGL((k_bwd_coop<KK, true, false>), dim3(blocks), dim3(64 * NWC), 0, s, g, a); \
+        if (win)                                                                                         \
+            hipLaunchKernelGGL((k_bwd_coop<KK, true>), dim3(blocks), dim3(64 * NWC), 0, s, g, a);        \
         else                                                                                             \
-            hipLaunchKernelGGL((k_bwd_coop<KK, false, false>), dim3(blocks), dim3(64 * NWC), 0, s, g, a); \
+            hipLaunchKernelGGL((k_bwd_coop<KK, false>), dim3(blocks), dim3(64 * NWC), 0, s, g, a);       \
         break;
             CUSTMA_SWEEP_KS(CUSTMA_K)
 #undef CUSTMA_K
             default: return hipErrorInvalidValue;
         }
         prof_end(PROF_BWD, s);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (p.rem) {
+        switch (g.k) {
+#define CUSTMA_K(KK)                                                                                             \
+    case KK:                                                                                                            \
+        hipLaunchKernelGGL((k_bwd_rem_rows<KK>), dim3((unsigned)cdiv(rem_units, 4)), dim3(256), 0, s, g, a, rem_tiles); \
+        break;
+            CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+            default: return hipErrorInvalidValue;
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     // (gather and combine fused into one tiled pass -- the slot sums recomputed for each tile's r
