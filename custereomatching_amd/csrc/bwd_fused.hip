@@ -230,8 +230,8 @@ __device__ __forceinline__ float reduce_tail3(float w0, float w1, float w2, int 
 // of three stays below 2^32); in-range offsets stay below kWinNR (win_path_ok).
 constexpr uint32_t kWinNR = 0x55555550u;
 
-template <int N>
-__device__ __forceinline__ float tree_sum(const float* c) {
+template <int N, typename F>
+__device__ __forceinline__ F tree_sum(const F* c) {
     if constexpr (N == 1) return c[0];
     else return tree_sum<N / 2>(c) + tree_sum<N - N / 2>(c + N / 2);
 }
@@ -651,20 +651,29 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 // in 64, or light units whose lanes are unit rows (eight loads per step, each lane a different
 // line of the gradient, the volume and the six prepared images: 445 M line requests per C5 launch
 // beside the sweep's ~1 G), both cost k_bwd_coop ~4 ms at C5 (20.8 ms without the diagonal,
-// profiles/r03/rem).  k_bwd_rem_rows instead walks ROWS with lanes = 64 consecutive camera
-// columns w: per step (volume row h) two strided loads (gradient and volume at diagonal D: one
-// line per lane, unavoidable), the prepared-image values coalesced, A_D and V_D, the vertical box
-// of A_D as a K-deep sliding sum in registers (the row loop unrolled K times), the horizontal box
-// through a wave-private LDS row (no barrier), and the six terms stored per row (a.remT / a.remT1,
-// added by k_bwd_gather).  A wave owns the 64 - 2R middle columns of its 64 (the outer R on each
-// side only feed the horizontal box); one wave per (column tile, row band).  Same fp32 arithmetic
-// as the sweep's other diagonals.
+// profiles/r03/rem); so does copying the two values out in the last chunk's sweep (two more
+// lane-masked loads per step: +1.8 ms, the sweep is bound by its line requests).
+// k_bwd_rem_rows instead walks ROWS with lanes = 64 consecutive camera columns w: per step (volume
+// row h) ONE strided load (the gradient at diagonal D: one line per lane, unavoidable), the
+// prepared-image values coalesced, A_D and V_D, the vertical box of A_D as a K-deep sliding sum (ring in
+// LDS), the horizontal box through a wave-private LDS row (no
+// barrier), and the six terms stored per row (a.remT / a.remT1, added by k_bwd_gather).
+// The cost of diagonal D is recomputed from the images instead of read from the volume (a second
+// line per voxel; the reference's backward recomputes every voxel's cost, stereo_matching_kernel.cu:
+// 97-151): E + eps = sum c p - box_c box_p / k^2 + eps in fp64 (the products of row h + R enter a
+// K-deep ring of their horizontal box sums, so the patch sum is exact for fp16 inputs and within
+// the forward's own fp64 arithmetic for fp32), cost = (float)(E + eps) rsq(X Y + eps) with the
+// same fp32 moments as A_D.  A wave owns the 64 - 2R middle columns of its 64 (the outer R on each
+// side only feed the horizontal boxes); one wave per (column tile, row band).
 constexpr int kRemRB = 64;  // output rows per row band
 
 template <int K>
 __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntile) {
     constexpr int R = K / 2, OWN = 64 - 2 * R;
     __shared__ float xs_[4][64];
+    __shared__ double xp_[4][64];
+    __shared__ float ringA_[4][K * 64];
+    __shared__ double ringP_[4][K * 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t unit = (int64_t)blockIdx.x * 4 + wv;
     const int tile = (int)(unit % ntile);
@@ -681,11 +690,12 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
     const float cb = a.shift[0], pb = a.shift[1];
     const uint32_t pb4 = (uint32_t)(plane * 4);
     enum { kX = 0, kMc = 1, kC = 2, kY = 3, kMp = 4, kP = 5 };
-    // volume rows of this band: [y0 - R, y1 + R) clipped to [h_lo, h_hi); offsets relative to vb
+    // gradient rows of this band: [y0 - R, y1 + R) clipped to [h_lo, h_hi); offsets relative to vb
     const int vb = (int)max((int64_t)hlo, y0 - R);
     const auto rG = make_rsrc(a.grad + (size_t)(vb - hlo) * slab, 0x7FFFFFF0u);
-    const auto rV = make_rsrc(a.vol + (size_t)(vb - hlo) * slab, 0x7FFFFFF0u);
     const auto rP = make_rsrc(a.Xc, 0x7FFFFFF0u);
+    const auto rBc = make_rsrc(a.sc.box, (uint32_t)min((size_t)0x7FFFFFF0u, plane * 8));
+    const auto rBp = make_rsrc(a.sp.box, (uint32_t)min((size_t)0x7FFFFFF0u, plane * 8));
     constexpr uint32_t OOB = 0x80000000u;
     const uint32_t vcol = wok ? (uint32_t)((size_t)w * g.DO + Di) * 4u : OOB;  // voxel (., w, D) in a row
     const uint32_t vstride = (uint32_t)(slab * 4);
@@ -693,67 +703,105 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
     const auto rT = make_rsrc(a.remT, (uint32_t)(4 * nvR * 4));
     const auto rT1 = make_rsrc(a.remT1, (uint32_t)(2 * nywR * 4));
     float* xs = xs_[wv];
-    struct Ld { float g, v, x, y, mp, mc; };
-    // loads of volume row h (zero outside the volume rows / columns: A_D = 0 there)
+    double* xp = xp_[wv];
+    const double rk2 = 1.0 / (double)(K * K);
+    struct Ld { float g, x, y, mp, mc, c, p; double bc, bp; };
+    // loads of volume row h (zero outside the volume rows / columns: A_D = 0 there) and the raw
+    // images of row h + R (the product row that enters the patch sums at step h)
     auto load = [&](int h, Ld& b) {
         const bool hv = h >= hlo && h < hhi, hi = h >= 0 && h < Hi;
         const uint32_t vo = hv && vcol != OOB ? (uint32_t)(h - vb) * vstride + vcol : OOB;
         const uint32_t io = hi ? (uint32_t)(h * Wi) * 4u : OOB;
         b.g = ld_buf<float>(rG, vo);
-        b.v = ld_buf<float>(rV, own ? vo : OOB);
         b.x = ld_buf<float>(rP, io != OOB && w >= 0 && w < Wi ? io + (uint32_t)w * 4u + kX * pb4 : OOB);
         b.y = ld_buf<float>(rP, io != OOB && wok ? io + (uint32_t)(w + Di) * 4u + kY * pb4 : OOB);
-        b.mp = ld_buf<float>(rP, io != OOB && wok && own ? io + (uint32_t)(w + Di) * 4u + kMp * pb4 : OOB);
-        b.mc = ld_buf<float>(rP, io != OOB && wok && own ? io + (uint32_t)w * 4u + kMc * pb4 : OOB);
+        const bool ow = io != OOB && wok && own;
+        b.mp = ld_buf<float>(rP, ow ? io + (uint32_t)(w + Di) * 4u + kMp * pb4 : OOB);
+        b.mc = ld_buf<float>(rP, ow ? io + (uint32_t)w * 4u + kMc * pb4 : OOB);
+        b.bc = ld_buf_f64(rBc, ow ? (uint32_t)(h * Wi + w) * 8u : OOB);
+        b.bp = ld_buf_f64(rBp, ow ? (uint32_t)(h * Wi + w + Di) * 8u : OOB);
+        const int he = h + R;
+        const bool ei = he >= 0 && he < Hi;
+        const uint32_t eo = (uint32_t)(he * Wi) * 4u;
+        b.c = ld_buf<float>(rP, ei && w >= 0 && w < Wi ? eo + (uint32_t)w * 4u + kC * pb4 : OOB);
+        b.p = ld_buf<float>(rP, ei && w + Di >= 0 && w + Di < Wi ? eo + (uint32_t)(w + Di) * 4u + kP * pb4 : OOB);
     };
-    float ring[K];  // A_D of the last K rows (slot = step mod K)
+    // horizontal box over the lanes x - R .. x + R of a product row (own lanes)
+    auto hbox = [&](double v) {
+        xp[lane] = v;
+        double c[2 * R + 1];
 #pragma unroll
-    for (int i = 0; i < K; ++i) ring[i] = 0.f;
-    float VS = 0.f;  // vertical sum of A_D over rows h - K + 1 .. h
+        for (int j = 0; j <= 2 * R; ++j) c[j] = xp[own ? lane - R + j : 0];
+        return tree_sum<2 * R + 1>(c);
+    };
+    // the two K-deep rings in LDS (wave-private; a register ring needs the row loop unrolled K times,
+    // and then the compiler keeps every step's horizontal-box operands live: 270+ VGPRs at k = 11)
+    float* ring = ringA_[wv];    // [K][64] A_D of the last K rows (slot = step mod K)
+    double* ringP = ringP_[wv];  // [K][64] horizontal box sums of c p of the last K product rows
+#pragma unroll
+    for (int i = 0; i < K; ++i) { ring[i * 64 + lane] = 0.f; ringP[i * 64 + lane] = 0.0; }
+    float VS = 0.f;   // vertical sum of A_D over rows h - K + 1 .. h
+    double SP = 0.0;  // patch sum of c p at (h, w): the product rows h - R .. h + R
     const int hs = (int)(y0 - R), he = (int)(y1 + R);  // rows walked; output y = h - R for y in [y0, y1)
+    // warm-up: product rows hs - R .. hs + R - 1 into slots 1 .. K - 1 (step t puts row hs + t + R
+    // into slot t mod K, evicting row hs + t - R - 1)
+    for (int jj = 0; jj < K - 1; ++jj) {
+        const int ry = hs - R + jj;
+        const bool ei = ry >= 0 && ry < Hi;
+        const uint32_t eo = (uint32_t)(ry * Wi) * 4u;
+        const float c = ld_buf<float>(rP, ei && w >= 0 && w < Wi ? eo + (uint32_t)w * 4u + kC * pb4 : OOB);
+        const float p = ld_buf<float>(rP, ei && w + Di >= 0 && w + Di < Wi ? eo + (uint32_t)(w + Di) * 4u + kP * pb4 : OOB);
+        const double pe = hbox((double)c * (double)p);
+        ringP[(jj + 1) * 64 + lane] = pe;
+        SP += pe;
+    }
     Ld cur, nxt;
     load(hs, cur);
-    for (int hb = hs; hb < he; hb += K) {
-        Unroll<0, K>::run([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            const int h = hb + i;
-            if (h < he) {
-                load(h + 1, nxt);  // past the band: in range or masked, unused
-                const float rSD = __builtin_amdgcn_rsqf(__builtin_fmaf(cur.x, cur.y, kEps));
-                const float AD = cur.g * rSD, VD = AD * cur.v * rSD;
-                VS += AD - ring[i];
-                ring[i] = AD;
-                // per-voxel terms of (h, w): stored by the lanes that own column w
-                if (own && wok && h >= hlo && h < hhi && h >= y0 && h < y1) {  // each row by one band
-                    const uint32_t tv = (uint32_t)(((int64_t)(h - hlo) * WOi + w) * 4), tn = (uint32_t)(nvR * 4);
-                    st_buf(AD * cur.mp, rT, tv);           // camera Am at (h, w):  A mp'(h, w + D)
-                    st_buf(VD * cur.y, rT, tv + tn);       // camera B  at (h, w):  V Y(h, w + D)
-                    st_buf(AD * cur.mc, rT, tv + 2 * tn);  // projector Ac at (h, w + D): A mc'(h, w)
-                    st_buf(VD * cur.x, rT, tv + 3 * tn);   // projector Bp at (h, w + D): V X(h, w)
-                }
-                // output row y = h - R: BoxA_D(y, x) = sum of VS over the lanes x - R .. x + R
-                const int y = h - R;
-                if (y >= y0) {
-                    xs[lane] = VS;
-                    float c[2 * R + 1];
+    int slot = 0;
+    for (int h = hs; h < he; ++h) {
+        load(h + 1, nxt);  // past the band: in range or masked, unused
+        {  // product row h + R enters, row h - R - 1 leaves (the forward's sliding fp64 sums)
+            const double pe = hbox((double)cur.c * (double)cur.p);
+            SP = (SP + pe) - ringP[slot * 64 + lane];
+            ringP[slot * 64 + lane] = pe;
+        }
+        const float rSD = __builtin_amdgcn_rsqf(__builtin_fmaf(cur.x, cur.y, kEps));
+        const float AD = cur.g * rSD;
+        VS += AD - ring[slot * 64 + lane];
+        ring[slot * 64 + lane] = AD;
+        slot = slot + 1 == K ? 0 : slot + 1;
+        // per-voxel terms of (h, w): stored by the lanes that own column w
+        if (own && wok && h >= hlo && h < hhi && h >= y0 && h < y1) {  // each row by one band
+            // E + eps = sum c p - box_c box_p / k^2 + eps (the forward's fin_bc form)
+            const double e = __builtin_fma(-cur.bc, cur.bp * rk2, SP + (double)kEps);
+            const float VD = AD * ((float)e * rSD) * rSD;
+            const uint32_t tv = (uint32_t)(((int64_t)(h - hlo) * WOi + w) * 4), tn = (uint32_t)(nvR * 4);
+            st_buf(AD * cur.mp, rT, tv);           // camera Am at (h, w):  A mp'(h, w + D)
+            st_buf(VD * cur.y, rT, tv + tn);       // camera B  at (h, w):  V Y(h, w + D)
+            st_buf(AD * cur.mc, rT, tv + 2 * tn);  // projector Ac at (h, w + D): A mc'(h, w)
+            st_buf(VD * cur.x, rT, tv + 3 * tn);   // projector Bp at (h, w + D): V X(h, w)
+        }
+        // output row y = h - R: BoxA_D(y, x) = sum of VS over the lanes x - R .. x + R
+        const int y = h - R;
+        if (y >= y0) {
+            xs[lane] = VS;
+            float c[2 * R + 1];
 #pragma unroll
-                    for (int j = 0; j <= 2 * R; ++j) c[j] = xs[own ? lane - R + j : 0];
-                    const float box = tree_sum<2 * R + 1>(c);
-                    const int x = w;  // output column of an own lane
-                    if (own) {
-                        const uint32_t ty = (uint32_t)((y - (int)a.ylo) * Wi * 4);
-                        const uint32_t yi = (uint32_t)(y * Wi) * 4u;
-                        // T1c at (y, x): p'(y, x + D) BoxA_D;  T1p at (y, x + D): c'(y, x) BoxA_D
-                        const int xd = x + Di;
-                        const float pv = ld_buf<float>(rP, xd >= 0 && xd < Wi ? yi + (uint32_t)xd * 4u + kP * pb4 : OOB);
-                        const float cv = ld_buf<float>(rP, x >= 0 && x < Wi ? yi + (uint32_t)x * 4u + kC * pb4 : OOB);
-                        if (x >= 0 && x < Wi) st_buf((pv - pb) * box, rT1, ty + (uint32_t)x * 4u);
-                        if (xd >= 0 && xd < Wi) st_buf((cv - cb) * box, rT1, (uint32_t)(nywR * 4) + ty + (uint32_t)xd * 4u);
-                    }
-                }
-                cur = nxt;
+            for (int j = 0; j <= 2 * R; ++j) c[j] = xs[own ? lane - R + j : 0];
+            const float box = tree_sum<2 * R + 1>(c);
+            const int x = w;  // output column of an own lane
+            if (own) {
+                const uint32_t ty = (uint32_t)((y - (int)a.ylo) * Wi * 4);
+                const uint32_t yi = (uint32_t)(y * Wi) * 4u;
+                // T1c at (y, x): p'(y, x + D) BoxA_D;  T1p at (y, x + D): c'(y, x) BoxA_D
+                const int xd = x + Di;
+                const float pv = ld_buf<float>(rP, xd >= 0 && xd < Wi ? yi + (uint32_t)xd * 4u + kP * pb4 : OOB);
+                const float cv = ld_buf<float>(rP, x >= 0 && x < Wi ? yi + (uint32_t)x * 4u + kC * pb4 : OOB);
+                if (x >= 0 && x < Wi) st_buf((pv - pb) * box, rT1, ty + (uint32_t)x * 4u);
+                if (xd >= 0 && xd < Wi) st_buf((cv - cb) * box, rT1, (uint32_t)(nywR * 4) + ty + (uint32_t)xd * 4u);
             }
-        });
+        }
+        cur = nxt;
     }
 }
 
@@ -994,7 +1042,9 @@ __global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict
 // grad(y,x) = T1 - Box[Z] - img'(y,x) Box[B]   (k_bwd_gather2's Z = A - m' B; one side per blockIdx.z)
 // TS x TS output tiles (TS = 32: the (TS + 2r)^2 input halo is 1.7x the tile, 2.6x at 16); inputs
 // staged as fp32 (they are stored so), row sums and column sums in fp64, fixed order.
-template <typename T, int TS>
+// KT > 0: the window size at compile time (the sweep's sizes: unrolled tap loops, constant tile
+// pitch; C5 0.72 -> 0.58 ms); KT = 0: runtime k.
+template <typename T, int TS, int KT = 0>
 __global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict__ cam, const T* __restrict__ proj,
                                                       const float* __restrict__ shift, const acc_t* __restrict__ acc,
                                                       float* __restrict__ dcam, float* __restrict__ dproj) {
@@ -1007,7 +1057,7 @@ __global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict
     const acc_t* T1 = acc + (size_t)side * 3 * plane;
     const acc_t* Zz = T1 + plane;
     const acc_t* Bb = Zz + plane;
-    const int r = g.r, L = TS + 2 * r;
+    const int k = KT > 0 ? KT : g.k, r = k / 2, L = TS + 2 * r;
     double* hZ = tl;                 // [L][TS] row sums
     double* hB = hZ + L * TS;
     float* tZ = (float*)(hB + L * TS);  // [L][L] inputs
@@ -1025,7 +1075,8 @@ __global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict
     for (int e = threadIdx.x; e < L * TS; e += 256) {
         const int ry = e / TS, cx = e % TS;
         double a = 0, b = 0;
-        for (int jx = 0; jx < g.k; ++jx) {
+#pragma unroll
+        for (int jx = 0; jx < k; ++jx) {
             const int f = ry * L + cx + jx;
             a += (double)tZ[f];
             b += (double)tB[f];
@@ -1040,7 +1091,8 @@ __global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict
         const int64_t y = y0 + ly, x = x0 + lx;
         if (y >= g.H || x >= g.W) continue;
         double sz = 0, sb = 0;
-        for (int i = 0; i < g.k; ++i) {
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
             const int f = (ly + i) * TS + lx;
             sz += hZ[f];
             sb += hB[f];
@@ -1320,9 +1372,21 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
         constexpr int TS3 = 32;
         const int L3 = TS3 + 2 * g.r;
         const size_t lds3 = sizeof(double) * 2 * L3 * TS3 + sizeof(float) * 2 * L3 * L3;
-        if ((e = allow_lds(k_bwd_combine3<T, TS3>, lds3)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k_bwd_combine3<T, TS3>), dim3((unsigned)cdiv(g.W, TS3), (unsigned)cdiv(g.H, TS3), 2),
-                           dim3(256), lds3, s, g, cam, proj, shift, acc, dcam, dproj);
+        const dim3 cgrid((unsigned)cdiv(g.W, TS3), (unsigned)cdiv(g.H, TS3), 2);
+        auto go = [&](auto kc) {
+            constexpr int KK = decltype(kc)::value;
+            if ((e = allow_lds(k_bwd_combine3<T, TS3, KK>, lds3)) != hipSuccess) return;
+            hipLaunchKernelGGL((k_bwd_combine3<T, TS3, KK>), cgrid, dim3(256), lds3, s, g, cam, proj, shift, acc, dcam,
+                               dproj);
+        };
+        switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: go(std::integral_constant<int, KK>{}); break;
+            CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+            default: go(std::integral_constant<int, 0>{});
+        }
+        if (e != hipSuccess) return e;
     }
 #endif
     return hipGetLastError();
