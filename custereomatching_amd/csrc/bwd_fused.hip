@@ -236,9 +236,27 @@ __device__ __forceinline__ F tree_sum(const F* c) {
     else return tree_sum<N / 2>(c) + tree_sum<N - N / 2>(c + N / 2);
 }
 
+// Camera values of a step (X of the own and halo rows at column w, mc' of the own rows, c at w - R)
+// from a wave-private LDS block instead of four per-step loads: one lane-per-column load of each of
+// the 12 + HP rows every 64 steps (a block ahead, like the sliding projector columns), written to
+// LDS at the block's first step, read back row-replicated (lane l: row l & 3) by four ds_reads per
+// step.  The per-step loads touched four lines each for 16 useful bytes (a third of the step's
+// line requests).  Only where the 3.9 KB per wave keeps the workgroups per CU (k = 11; k = 7, 9 and
+// 13 would drop one).
+template <int K>
+constexpr bool cam_lds_for() {
+#ifdef CUSTMA_BWD_CAMLDS
+    return CUSTMA_BWD_CAMLDS != 0 && K == 11;
+#else
+    return K == 11;
+#endif
+}
+constexpr int kCamP = 65;  // LDS row pitch of the camera block (65: the four rows of a read in different banks)
+
 template <int K, bool WIN>
 __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, int j, int sg, int rg, float* Abuf,
-                                              float* ring, float (*cbuf)[12], float (*pbuf)[12]) {
+                                              float* ring, float (*cbuf)[12], float (*pbuf)[12], float* camb) {
+    constexpr bool CAML = cam_lds_for<K>();
     constexpr int R = K / 2, NY = TRB + 2 * R, NH = 2 * R;  // NH halo rows
     constexpr int FBC = fbc_for<K>();
     static_assert(FBC % (BDP + 1) == 0 && FBC <= 16, "flush blocks start on load buffer 0; 4 FBC lanes");
@@ -314,7 +332,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         return make_rsrc(a.part + ((size_t)t * a.S + slot) * plane + (size_t)(y0 + yw) * g.W, prow_bytes);
     };
     // loads per issue() (asm_ld2s / asm_ld1s / asm_ld4), per thread
-    constexpr int NLD = (SLIDE ? TRW * 2 + (HPW > 0 ? HPW : 1) : TRW * 5 + (HPW > 0 ? HPW : 1) * 2) + 4;
+    constexpr int NLD = (SLIDE ? TRW * 2 + (HPW > 0 ? HPW : 1) : TRW * 5 + (HPW > 0 ? HPW : 1) * 2) + (CAML ? 0 : 4);
     auto flush = [&](int wfirst, int nsteps) {
         if constexpr (BDP == 2) asm_vmcnt<NLD>();  // all but the newest issue
         int ln = lane;
@@ -415,7 +433,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], vLane, vLane, dG, dV, sVo[m] + sW, sVo[m] + sW);
 #pragma unroll
             for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], vLane, dG, sVh[i] + sW);
-            asm_ld4s<NOP>(b.xo, b.xh, b.mc, b.cx, vXo, vXh, vMo, vCo, dPc, sC, sX);
+            if constexpr (!CAML) asm_ld4s<NOP>(b.xo, b.xh, b.mc, b.cx, vXo, vXh, vMo, vCo, dPc, sC, sX);
             return;
         }
         const bool ve = w >= lwlo && w < lwhi;
@@ -443,6 +461,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
                 asm_ld2s<NOP>(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dPr, sVh[i], sIh[i]);
             }
         }
+        if constexpr (!CAML)
         asm_ld4<NOP>(b.xo, b.xh, b.mc, b.cx, img_off_a(orow_l, w, kX), hrow_l >= 0 ? img_off_a(hrow_l, w, kX) : kOOB,
                 img_off_a(orow_l, w, kMc), img_off_a(orow_l, xb, kC), dPr, dPr, dPr);
     };
@@ -460,7 +479,27 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 #pragma unroll
         for (int i = 0; i < HP; ++i) asm_ld1s(hY[i], wv + NWC * i < NH ? oY : kOOB, dPr, sIh[i]);
     };
+    // CAML: the camera block registers (lane i: column wb + i of own row m's X / mc' (3m, 3m + 1),
+    // column wb - R + i of its c (3m + 2); halo row i's X at 12 + i), loaded a block ahead
+    constexpr int NCB = CAML ? 12 + HP : 1;
+    uint32_t cbk[NCB];
+    auto load_cam = [&](int wb) {
+        if constexpr (CAML) {
+            const uint32_t oX = col_off_a(wb + lane, kX), oM = col_off_a(wb + lane, kMc), oC = col_off_a(wb - R + lane, kC);
+#pragma unroll
+            for (int m = 0; m < TRW; ++m) {
+                asm_ld2s(cbk[3 * m], cbk[3 * m + 1], oX, oM, dPr, dPr, sIo[m], sIo[m]);
+                asm_ld1s(cbk[3 * m + 2], oC, dPr, sIo[m]);
+            }
+#pragma unroll
+            for (int i = 0; i < HP; ++i) asm_ld1s(cbk[12 + i], wv + NWC * i < NH ? oX : kOOB, dPr, sIh[i]);
+        }
+    };
     auto tie_cols = [&]() {
+        if constexpr (CAML) {
+#pragma unroll
+            for (int r = 0; r < NCB; ++r) asm_tie(cbk[r]);
+        }
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
             asm_tie(sc[3 * m]); asm_tie(sc[3 * m + 1]); asm_tie(sc[3 * m + 2]);
@@ -482,7 +521,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             if constexpr (!SLIDE) asm_tie(b.hY[i]);
         }
         asm_tie(b.xo); asm_tie(b.xh); asm_tie(b.mc); asm_tie(b.cx);
-        if constexpr (SLIDE) tie_cols();
+        if constexpr (SLIDE || CAML) tie_cols();
     };
     auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
 
@@ -530,6 +569,22 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             // issued after this step's reads of the previous block
             if (((w - w0) & 63) == 0) load_cols(bc, bhY, w + 64);
         }
+        uint32_t cxo_r = cur.xo, cxh_r = cur.xh, cmc_r = cur.mc, ccx_r = cur.cx;
+        if constexpr (CAML) {
+            typedef __attribute__((address_space(3))) float lds_f;
+            lds_f* cl = (lds_f*)camb;
+            const int cc = (w - w0) & 63;
+            if (cc == 0) {  // the block of steps w .. w + 63 into LDS, then the next block's loads
+#pragma unroll
+                for (int r = 0; r < NCB; ++r) cl[r * kCamP + lane] = F(cbk[r]);
+                load_cam(w + 64);
+            }
+            const int q = lane & 3;
+            cxo_r = __builtin_bit_cast(uint32_t, cl[(3 * q) * kCamP + cc]);
+            cmc_r = __builtin_bit_cast(uint32_t, cl[(3 * q + 1) * kCamP + cc]);
+            ccx_r = __builtin_bit_cast(uint32_t, cl[(3 * q + 2) * kCamP + cc]);
+            cxh_r = __builtin_bit_cast(uint32_t, cl[(12 + (q < HP ? q : HP - 1)) * kCamP + cc]);
+        }
         issue(w + BDP, nxt, std::false_type{});  // past the segment's end: harmless, drained before the wave ends
         float* Acur = Abuf + (NAB == 2 ? ((w - w0) & 1) * (NY * 64) : 0);
         // this wave's ring slot of the step (V of its rows K steps ago): wave-private, so read
@@ -544,8 +599,8 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         }
         const int xb = w - R;
         const float tf = xb >= xs ? 1.f : 0.f, af = (w >= xs && w < xe) ? 1.f : 0.f;
-        const float mco = F(cur.mc) * af;
-        const float cxo = (F(cur.cx) - cb) * tf;
+        const float mco = F(cmc_r) * af;
+        const float cxo = (F(ccx_r) - cb) * tf;
         // ---- own rows: A, and the per-voxel terms (unit rows R + yw .. R + yw + 3); the
         // row's camera values come from quad slot m of the row-replicated registers ----
         float amv[TRW], bv[TRW];
@@ -553,7 +608,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
             const int y = R + yw + m;
-            const float Xf = rbc<m>(F(cur.xo)), Ye = F(SLIDE ? sc[3 * m] : cur.Ye[m]);
+            const float Xf = rbc<m>(F(cxo_r)), Ye = F(SLIDE ? sc[3 * m] : cur.Ye[m]);
             const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, Ye, kEps));
             const float Ae = F(cur.ge[m]) * rSe;
             Acur[y * 64 + lane] = Ae;
@@ -569,7 +624,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             if (q < NH) {
                 const int y = halo_row(q);
                 Acur[y * 64 + lane] = F(cur.hg[i]) * __builtin_amdgcn_rsqf(
-                                                         __builtin_fmaf(rbc<i>(F(cur.xh)), F(SLIDE ? shY[i] : cur.hY[i]), kEps));
+                                                         __builtin_fmaf(rbc<i>(F(cxh_r)), F(SLIDE ? shY[i] : cur.hY[i]), kEps));
             }
         });
         if (s > 0) reduce_to(s - 1);
@@ -605,6 +660,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 
     Ld L[BDP + 1];
     if constexpr (SLIDE) load_cols(sc, shY, w0);  // the first step's columns, all lanes
+    load_cam(w0);  // CAML: the first block (written to LDS at step w0)
     issue(w0, L[0], std::true_type{});
     if constexpr (BDP == 2) issue(w0 + 1, L[1], std::true_type{});
     for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
@@ -633,7 +689,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     asm_vmcnt<0>();
 #pragma unroll
     for (int i = 0; i <= BDP; ++i) tie(L[i]);
-    if constexpr (SLIDE) tie_cols();
+    if constexpr (SLIDE || CAML) tie_cols();
     // ---- final projector state: lane l holds column (wend - 1) + off + d0 + l
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
@@ -848,8 +904,10 @@ __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, Bwd
     constexpr int FBC = fbc_for<K>();
     __shared__ __attribute__((aligned(16))) float cbuf[NWC][FBC][12];
     __shared__ __attribute__((aligned(16))) float pbuf[NWC][FBC][12];
+    constexpr int HPW = (2 * (K / 2) + NWC - 1) / NWC;
+    __shared__ float camL[NWC][cam_lds_for<K>() ? (12 + (HPW > 0 ? HPW : 1)) * kCamP : 1];
     const int wv = threadIdx.x >> 6;
-    bwd_coop_body<K, WIN>(g, a, j, sg, rg, Abuf, ring + wv * (K * TRW * 64), cbuf[wv], pbuf[wv]);
+    bwd_coop_body<K, WIN>(g, a, j, sg, rg, Abuf, ring + wv * (K * TRW * 64), cbuf[wv], pbuf[wv], camL[wv]);
 }
 
 // Per (range class, column): the partial slots that hold the column (class 0 = camera
