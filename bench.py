@@ -178,8 +178,16 @@ def north_star(steps, warmup):
     k, D = 11, 256
     cam, proj = synth_pair(H, W, D, 77, "cuda", torch.float16)
     out = cm.cost_volume_forward(cam, proj, D, k, "window", "fast")
-    for _ in range(warmup):
+    # Warm up to the steady state: the GPU's clocks ramp up over the first ~20 back-to-back launches
+    # after any idle gap (1.3-1.5 ms per op, settling at ~1.0 ms; scripts/throttle_probe.py,
+    # profiles/r03/dpm/), so at least `warmup` launches AND 0.25 s of back-to-back launches first.
+    t0 = time.perf_counter()
+    n = 0
+    while n < warmup or time.perf_counter() - t0 < 0.25:
         cm.cost_volume_forward(cam, proj, D, k, "window", "fast", out=out)
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize()
     et = EventTimer()
     _lib.profile_enable(True)
     for _ in range(steps):
@@ -215,7 +223,11 @@ def config2_step(steps):
         proj.grad = None
         cm.stereo_matching(cam, proj, D, k).backward(g)
 
-    step()
+    # steady-state clocks first (see north_star): 0.25 s of back-to-back steps
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.25:
+        step()
+        torch.cuda.synchronize()
     et = EventTimer()
     for _ in range(steps):
         et.record(step)
@@ -461,7 +473,7 @@ def main():
     torch.cuda.empty_cache()
     if rank == 0 and world == 1:
         if not args.no_north_star:
-            result["north_star"] = north_star(max(5, args.steps), 2)
+            result["north_star"] = north_star(max(20, args.steps), 40)
         if not args.no_config2 and args.workload != "c2":
             result["config2"] = config2_step(max(5, args.steps // 2))
         torch.cuda.empty_cache()

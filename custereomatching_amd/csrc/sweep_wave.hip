@@ -95,11 +95,17 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         return (have && x >= 0 && x < g.W) ? (uint32_t)(x * esz) : OOB;
     };
     const int64_t xO0 = u0 - R + d0, oS = u0 + d0;
-    const uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 64, xO0 + 64 + l, sizeof(T));
-    const uint32_t vC0 = colOff(true, u0 - R + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R + 16 + r16, sizeof(T));
-    const uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 64, oS + 64 + l, 8);
-    const uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 64, oS + 64 + l, 4);
-    const uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
+    uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 64, xO0 + 64 + l, sizeof(T));
+    uint32_t vC0 = colOff(true, u0 - R + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R + 16 + r16, sizeof(T));
+    uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 64, oS + 64 + l, 8);
+    uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 64, oS + 64 + l, 4);
+    uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
+#ifdef CUSTMA_ABL_NOSTATSMEM  // ablation (timing only): statistics loads out of range (no memory access)
+    vM0 = vM1 = vQ0 = vQ1 = vUB = vUQ = OOB;
+#endif
+#ifdef CUSTMA_ABL_NOIMGMEM  // ablation (timing only): image-row loads out of range
+    vP0 = vP1 = vC0 = vC1 = OOB;
+#endif
     // Rows by SGPR soffset from one descriptor per array, based at the band's first row rb
     // (so every offset stays small whatever the image size); a row outside the image gets
     // soffset OOBS, past num_records (<= OOBS), so its loads read 0 -- also when the lane's
@@ -520,14 +526,15 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     // SS stores per thread cover the 16 DO-float block: DO <= 64 nChunk, or 64 nChunk + 1 (rem);
     // X4: 4 (5 with rem) 16-byte stores per thread
     constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
+    constexpr int kTP = X4 ? kTileP : 2;  // deeper pipelines only with the 16-byte stores (vmcnt range)
     if (!wg.rem)
-        wave_body<K, T, false, false, true, S0, kTileP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
+        wave_body<K, T, false, false, true, S0, kTP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
                                                              sQ, sR, stage, part);
     else if (w == wg.nChunk - 1)
-        wave_body<K, T, false, true, true, S1, kTileP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
+        wave_body<K, T, false, true, true, S1, kTP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
                                                             sQ, sR, stage, part);
     else
-        wave_body<K, T, false, false, true, S1, kTileP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
+        wave_body<K, T, false, false, true, S1, kTP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
                                                              sQ, sR, stage, part);
 }
 

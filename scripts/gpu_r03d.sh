@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU tests (-k filter) then a per-kernel A/B with env switches on the same library.
+# Usage: bash scripts/gpu_r03d.sh <tag> <cfgs> <ops> "<pytest -k expr>" "<name>:<variant|base>:<ENV=V,...>" ...
+set -o pipefail
+TAG=$1; CFG=$2; OPS=$3; KX=$4; shift 4
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/$TAG
+mkdir -p $O
+if [ -n "$KX" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "$KX" > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
+  tail -1 $O/gpu_tests.log
+fi
+bash scripts/gpu_kprof.sh $TAG $CFG $OPS "$@"

@@ -17,6 +17,14 @@ CFGS = {
     "c3_win_k16": dict(H=2048, W=2048, k=16, D=256, layout="window", dtype=torch.float16),
 }
 
+def warm(fn, secs=0.25):
+    """Back-to-back launches until the clocks have ramped up (scripts/throttle_probe.py)."""
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < secs:
+        fn()
+        torch.cuda.synchronize()
+
+
 def run(name, ops, reps):
     c = CFGS[name]
     H, W, k, D, lay, dt = c["H"], c["W"], c["k"], c["D"], c["layout"], c["dtype"]
@@ -25,6 +33,7 @@ def run(name, ops, reps):
     if "fwd" in ops or "exact" in ops:
         for prec in [p for p in ("fast", "exact") if (p == "fast" and "fwd" in ops) or (p == "exact" and "exact" in ops)]:
             out = cm.cost_volume_forward(cam, proj, D, k, lay, prec)
+            warm(lambda: cm.cost_volume_forward(cam, proj, D, k, lay, prec, out=out))
             et = EventTimer()
             _lib.profile_enable(True)
             for _ in range(reps):
@@ -40,7 +49,7 @@ def run(name, ops, reps):
     if "bwd" in ops:
         vol = cm.cost_volume_forward(cam, proj, D, k, lay, "fast")
         g = torch.rand_like(vol) - 0.5
-        cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True, cost_volume=vol)
+        warm(lambda: cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True, cost_volume=vol))
         et = EventTimer()
         for _ in range(reps):
             et.record(lambda: cm.cost_volume_backward(g, cam, proj, k, lay, D, projector_grad=True,
@@ -50,7 +59,7 @@ def run(name, ops, reps):
         res["bwd_GBps_g_vol"] = round(2 * g.numel() * 4 / ms / 1e6, 1)
         del g, vol
     if "disp" in ops:
-        cm.stereo_disparity(cam, proj, D, k, lay)
+        warm(lambda: cm.stereo_disparity(cam, proj, D, k, lay))
         et = EventTimer()
         nre = None
         for _ in range(reps):
@@ -58,7 +67,7 @@ def run(name, ops, reps):
         res["disp_ms"] = round(et.mean_ms(), 4)
         res["disp_rechecked"] = int(nre[2].item())
     if "soft" in ops:
-        cm.stereo_disparity_soft(cam, proj, D, k, lay)
+        warm(lambda: cm.stereo_disparity_soft(cam, proj, D, k, lay))
         et = EventTimer()
         for _ in range(reps):
             et.record(lambda: cm.stereo_disparity_soft(cam, proj, D, k, lay))
