@@ -174,8 +174,12 @@ inline SweepGrid sweep_grid(const Geo& g, bool owned = false) {
         if (!owned && g.layout != CUSTMA_LAYOUT_WINDOW && nw > 4) continue;
         const int64_t per = owned ? 64 * nw - margin : 64 * nw;
         const int64_t n = owned ? cdiv(ncol, per) : cdiv(nd, per);
-        const double cost = (double)(n * 64 * nw) * (nw == 1 ? 1.1 : 1.0) * (nw == 5 ? 1.05 : 1.0);
-        if (cost < best) { best = cost; sg.NL = 64 * nw; }
+        // the disparity partials (!owned): 3-wave chunks run best where lane counts tie (C2 full:
+        // 1.98 ms against 2.39 for 2 waves and 3.06 for 4, profiles/r03/disp2), so ties go to more
+        // waves and 4 waves pay 10 %
+        const double cost = (double)(n * 64 * nw) * (nw == 1 ? 1.1 : 1.0) * (nw == 5 ? 1.05 : 1.0) *
+                            (!owned && nw == 4 ? 1.1 : 1.0);
+        if (cost < best || (!owned && cost == best)) { best = cost; sg.NL = 64 * nw; }
     }
     sg.S = owned ? sg.NL - margin : sg.NL;
     sg.nChunk = (int)(owned ? cdiv(ncol, (int64_t)sg.S) : cdiv(nd, (int64_t)sg.NL));

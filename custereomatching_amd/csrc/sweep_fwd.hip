@@ -341,6 +341,11 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             float qv[TWT];
 #pragma unroll
             for (int m = 0; m < TWT; ++m) { mv[m] = mrow[m]; qv[m] = qrow[m]; }
+            // ARGMAX: tile rows at pitch NL + TPR (the reduction's TPR-lane groups read column m's row
+            // at banks m TPR + lane: conflict-free)
+            int TPR = 1;
+            while (TPR * 2 * TWT <= NL && TPR < 16) TPR *= 2;
+            const int NLP = ARGMAX ? NL + TPR : NL;
             float* srow = stg + (ARGMAX ? 0 : buf * 16 * NL) + tid;
             // DIRECT (window layout, one chunk of diagonals): lane tid holds volume column
             // d0 + tid of the 16 rows u0 .. u0+15, so each m is one 256-byte store from the
@@ -355,7 +360,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 fmac_bc32<m>(den2, uq, qv[m]);              // ex2 * ey2 + eps
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
                 if constexpr (ARGMAX) {
-                    srow[m * NL] = (m >= m_lo && m < m_hi) ? c : -FLT_MAX;
+                    srow[m * NLP] = (m >= m_lo && m < m_hi) ? c : -FLT_MAX;
                 } else if constexpr (DIRECT) {
                     if (h >= h0) st_vol(c, rOutD, dvoff[m]);
                 } else {
@@ -364,10 +369,10 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             });
             if constexpr (ARGMAX) {
                 __syncthreads();
-                // TPR threads per camera column (power of two), PER diagonals each, in order
-                int TPR = 1;
-                while (TPR * 2 * TWT <= NL && TPR < 16) TPR *= 2;
-                const int PER = (NL + TPR - 1) / TPR;
+                // TPR lanes per camera column (a power of two, TPR x 16 <= NL), each scanning the
+                // diagonals l = part_i + TPR e in increasing order (branch-free: the first index wins
+                // among equal values), then the TPR lanes combined by DPP (quad xor 1, xor 2, half-row
+                // mirror, row mirror: each lane meets every other lane's part once)
                 const int m = tid / TPR, part_i = tid % TPR;
                 const bool red_live = m < TWT;
                 float best = -FLT_MAX, second = -FLT_MAX, q0 = 0.f, q1 = 0.f;
@@ -375,27 +380,37 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 const bool soft = part.s0 != nullptr;
                 // layout index s of diagonal lane l for camera column u0 + m
                 const float sbase = (float)(window ? d0 : u0 + m + d0);
-                for (int e = 0; red_live && e < PER; ++e) {
-                    const int l = part_i * PER + e;
-                    if (l >= NL) break;
-                    const float v = stg[m * NL + l];
+                const float* rowp = stg + (red_live ? m : 0) * NLP;
+#pragma unroll 4
+                for (int l = part_i; l < NL; l += TPR) {
+                    const float v = red_live ? rowp[l] : -FLT_MAX;
                     if (soft && v > -FLT_MAX) soft_add(v, sbase + (float)l, best, part.kb, q0, q1);
-                    if (v > best) { second = best; best = v; bi = l; }
-                    else if (v > second) second = v;
+                    const bool gt = v > best;
+                    second = gt ? best : fmaxf(second, v);
+                    bi = gt ? l : bi;
+                    best = gt ? v : best;
                 }
-                for (int off = 1; off < TPR; off <<= 1) {
-                    const float ob = __shfl_xor(best, off), os = __shfl_xor(second, off);
-                    const int oi = __shfl_xor(bi, off);
-                    if (soft) {
-                        const float o0 = __shfl_xor(q0, off), o1 = __shfl_xor(q1, off);
-                        soft_merge(best, ob, o0, o1, part.kb, q0, q1);
-                    }
+                auto merge = [&](auto ctl) {
+                    constexpr int c = decltype(ctl)::value;
+                    auto mv = [&](float x) {
+                        return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), c,
+                                                                                     0xf, 0xf, false));
+                    };
+                    const float ob = mv(best), os = mv(second);
+                    const int oi = __builtin_amdgcn_update_dpp(0, bi, c, 0xf, 0xf, false);
+                    if (soft) soft_merge(best, ob, mv(q0), mv(q1), part.kb, q0, q1);
                     if (ob > best || (ob == best && oi < bi)) {
-                        second = fmaxf(os, best); best = ob; bi = oi;
+                        second = fmaxf(os, best);
+                        best = ob;
+                        bi = oi;
                     } else {
                         second = fmaxf(second, ob);
                     }
-                }
+                };
+                if (TPR >= 2) merge(std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+                if (TPR >= 4) merge(std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+                if (TPR >= 8) merge(std::integral_constant<int, 0x141>{});  // row_half_mirror
+                if (TPR >= 16) merge(std::integral_constant<int, 0x140>{}); // row_mirror
                 const int64_t u = u0 + m;
                 if (red_live && part_i == 0 && u < g.WO) {
                     const int64_t pidx = ((int64_t)chunk * g.HV() + (h - g.h_lo)) * g.WO + u;
@@ -449,7 +464,7 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
     constexpr int NL_MAX = 320, OP = 64 * ((NX + NL_MAX - 1 + 63) / 64), SP = 64 * ((TW + NL_MAX - 1 + 63) / 64);
     const int NL = sg.NL;
     const size_t lds = sizeof(double) * (4 * OP + 2 * 64 + 2 * SP + 2 * 64) +
-                       sizeof(float) * (2 * SP + 2 * 64 + (direct ? 0 : (part ? 1 : 2) * TW * NL));
+                       sizeof(float) * (2 * SP + 2 * 64 + (direct ? 0 : part ? TW * (NL + 16) : 2 * TW * NL));
     const int64_t blocks = sweep_blocks(sg);
     if (part) {
         hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam,
