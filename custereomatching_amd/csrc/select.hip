@@ -141,6 +141,72 @@ __global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, c
     }
 }
 
+// k_disp_merge for window layouts with a compile-time window: one workgroup per 4 x 64 pixel tile
+// stages the camera tile and the projector strip its D + 1 diagonals reach (zero-padded, as float)
+// in LDS, so a certified pixel's exact best cost reads its two k x k patches from LDS instead of
+// 2 k^2 global loads (the projector patch at a per-pixel disparity).  Same fp32 operations in the
+// same order as exact_cost (bit-identical).
+constexpr int kMTY = 4, kMTX = 64;
+template <typename T, int KT>
+__global__ __launch_bounds__(256) void k_disp_merge_tile(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
+                                                         Stats sc, Stats sp, DispPartial part, int nChunk, float tau,
+                                                         int64_t* __restrict__ idx, float* __restrict__ best,
+                                                         int32_t* __restrict__ counter, int64_t* __restrict__ queue,
+                                                         SoftOut so, int ntx) {
+    constexpr int R = KT / 2, CY = kMTY + 2 * R, CX = kMTX + 2 * R;
+    extern __shared__ float tl[];
+    const int PX = kMTX + (int)g.D + 2 * R;  // projector strip width
+    float* tc = tl;
+    float* tp = tl + CY * CX;
+    const int64_t x0 = (int64_t)(blockIdx.x % ntx) * kMTX, hy0 = g.h_lo + (int64_t)(blockIdx.x / ntx) * kMTY;
+    for (int e = threadIdx.x; e < CY * CX; e += 256)
+        tc[e] = ldpad(cam, g.H, g.W, hy0 - R + e / CX, x0 - R + e % CX);
+    for (int e = threadIdx.x; e < CY * PX; e += 256)
+        tp[e] = ldpad(proj, g.H, g.W, hy0 - R + e / PX, x0 - R + e % PX);
+    __syncthreads();
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int64_t h = hy0 + ty, w = x0 + tx;
+    if (h >= g.h_hi || w >= g.WO) return;
+    const int64_t npix = g.HV() * g.WO, p = (h - g.h_lo) * g.WO + w;
+    float b = -FLT_MAX, sec = -FLT_MAX, q0 = 0.f, q1 = 0.f;
+    int64_t bi = INT64_MAX;
+    for (int c = 0; c < nChunk; ++c) {
+        const int64_t q = (int64_t)c * npix + p;
+        const int32_t oi = part.index[q];
+        if (oi < 0) continue;
+        const float ob = part.best[q], os = part.second[q];
+        if (so.soft) soft_merge(b, ob, part.s0[q], part.s1[q], so.kb, q0, q1);
+        if (ob > b || (ob == b && oi < bi)) {
+            sec = fmaxf(os, b); b = ob; bi = oi;
+        } else {
+            sec = fmaxf(sec, ob);
+        }
+    }
+    if (bi != INT64_MAX && (sec == -FLT_MAX || b - sec > tau)) {
+        idx[p] = bi;
+        const int64_t d = w + bi;  // window layout: d = w + s
+        const float mc = sc.mean[h * g.W + w], mp = sp.mean[h * g.W + d];
+        float e = 0.f;
+        const float* cr = tc + ty * CX + tx;
+        const float* pr = tp + ty * PX + tx + (int)bi;
+#pragma unroll
+        for (int i = 0; i < KT; ++i) {
+#pragma unroll
+            for (int j = 0; j < KT; ++j) e = __builtin_fmaf(cr[j] - mc, pr[j] - mp, e);
+            cr += CX;
+            pr += PX;
+        }
+        const float den = sqrtf(__builtin_fmaf(sc.sq[h * g.W + w], sp.sq[h * g.W + d], kEps));
+        const float eb = (e + kEps) / den;
+        if (best) best[p] = eb;
+        if (so.mask) so.mask[p] = eb > so.threshold ? 1.f : 0.f;
+        if (so.soft) so.soft[p] = q1 / q0;
+    } else {
+        const int32_t slot = atomicAdd(counter, 1);
+        queue[slot] = p;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_disp_recheck(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                       Stats sc, Stats sp, const int32_t* __restrict__ counter,
@@ -241,8 +307,26 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
     const float tau = (float)(8.0 * (g.k * g.k + 6) * 5.9604644775390625e-08);
     const int64_t npix = g.HV() * g.WO;
     const unsigned mb = (unsigned)cdiv(npix, 256);
+    // window layouts: the LDS-tiled merge while the projector strip fits
+    const int ntx = (int)cdiv(g.WO, kMTX);
+    const size_t mlds = sizeof(float) * (size_t)(kMTY + 2 * g.r) * (kMTX + 2 * g.r + (kMTX + g.D + 2 * g.r));
+    const bool mtile = g.layout == CUSTMA_LAYOUT_WINDOW && mlds <= 48 * 1024 && !getenv("CUSTMA_DISP_MERGE_FLAT");
+    const unsigned mtb = (unsigned)(ntx * cdiv(g.HV(), kMTY));
     auto merge = [&](auto kc) {
         constexpr int KT = decltype(kc)::value;
+        if constexpr (KT > 0) {
+            if (mtile) {
+                if (dtype == CUSTMA_F16)
+                    hipLaunchKernelGGL((k_disp_merge_tile<__half, KT>), dim3(mtb), dim3(256), mlds, s,
+                                       (const __half*)cam, (const __half*)proj, g, sc, sp, part, nChunk, tau, idx,
+                                       best, counter, queue, so, ntx);
+                else
+                    hipLaunchKernelGGL((k_disp_merge_tile<float, KT>), dim3(mtb), dim3(256), mlds, s,
+                                       (const float*)cam, (const float*)proj, g, sc, sp, part, nChunk, tau, idx,
+                                       best, counter, queue, so, ntx);
+                return;
+            }
+        }
         if (dtype == CUSTMA_F16)
             hipLaunchKernelGGL((k_disp_merge<__half, KT>), dim3(mb), dim3(256), 0, s, (const __half*)cam,
                                (const __half*)proj, g, sc, sp, part, nChunk, tau, idx, best, counter, queue, so);

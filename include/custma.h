@@ -85,6 +85,8 @@ int custma_forward(const void* camera, const void* projector, int32_t dtype, int
  * (custma/src/stereo_matching_kernel.cu:75-179, :218-261).  Deterministic (no atomics).
  * `cost_volume` is the forward's output for the same images (the autograd op keeps it); NULL makes
  * the call recompute it into the workspace (size the workspace with CUSTMA_OP_BACKWARD_RECOMPUTE).
+ * Window layouts with D = 64 n recompute the last diagonal's cost from the images rather than read
+ * it (one 128-byte line per voxel saved), as the reference recomputes every voxel's cost.
  * camera_grad / projector_grad may each be NULL (not computed); the reference computes the
  * camera gradient only (custma/stereo_matching_wrapper.py:33). */
 int custma_backward(const float* grad, const float* cost_volume, const void* camera, const void* projector,

@@ -46,8 +46,12 @@ VARIANTS = {
     "wait0vseq": (["CUSTMA_BWD_WAIT0", "CUSTMA_BWD_VSEQ"], BWD),
     "noslp": (["-fno-slp-vectorize"], BWD + ["stats.hip"]),  # no packed-fp32 pairing by the compiler
     "gather1": (["CUSTMA_BWD_GATHER1"], BWD),
-    # statistics tile: 16 x 64 pixels, 4 rows per thread is the default (32 x 8: C5 0.80 -> 0.98 ms)
-    "stats32x8": (["CUSTMA_STATS_TX=32", "CUSTMA_STATS_PR=8"], ["stats.hip"]),  # the per-pixel slot gather + 16x16 three-map combine  # round-3 step waits / vertical sum before  # fp64 per-pixel sums between gather and combine
+    # statistics tile: 32 x 32 pixels, 4 rows per thread is the default (profiles/r03/stats)
+    "stats32x8": (["CUSTMA_STATS_TX=32", "CUSTMA_STATS_PR=8"], ["stats.hip"]),
+    "stats16x8": (["CUSTMA_STATS_TX=16", "CUSTMA_STATS_PR=8"], ["stats.hip"]),
+    "stats32x4": (["CUSTMA_STATS_TX=32", "CUSTMA_STATS_PR=4"], ["stats.hip"]),
+    "stats64x2": (["CUSTMA_STATS_TX=64", "CUSTMA_STATS_PR=2"], ["stats.hip"]),
+    "stats16x2": (["CUSTMA_STATS_TX=16", "CUSTMA_STATS_PR=2"], ["stats.hip"]),  # the per-pixel slot gather + 16x16 three-map combine  # round-3 step waits / vertical sum before  # fp64 per-pixel sums between gather and combine
 }
 for n in (sys.argv[1:] or VARIANTS):
     d, only = VARIANTS[n]
