@@ -241,14 +241,17 @@ __device__ __forceinline__ F tree_sum(const F* c) {
 // the 12 + HP rows every 64 steps (a block ahead, like the sliding projector columns), written to
 // LDS at the block's first step, read back row-replicated (lane l: row l & 3) by four ds_reads per
 // step.  The per-step loads touched four lines each for 16 useful bytes (a third of the step's
-// line requests).  Only where the 3.9 KB per wave keeps the workgroups per CU (k = 11; k = 7, 9 and
-// 13 would drop one).
+// line requests).  k <= 11 (profiles/r03/caml: k = 5 -8 %, k = 9 -4..-5 % although the 3.9 KB per wave
+// costs k = 7, 9 their third workgroup per CU, k = 11 -4 %); k = 13 would drop to one workgroup per CU
+// (+54 %), k = 15, 17 are there already.
 template <int K>
 constexpr bool cam_lds_for() {
-#ifdef CUSTMA_BWD_CAMLDS
-    return CUSTMA_BWD_CAMLDS != 0 && K == 11;
+#ifdef CUSTMA_BWD_CAMLDS_ALL  // benchmarking: every kernel size (k = 7, 9, 13 then lose a workgroup per CU)
+    return true;
+#elif defined(CUSTMA_BWD_CAMLDS)
+    return CUSTMA_BWD_CAMLDS != 0 && K <= 11;
 #else
-    return K == 11;
+    return K <= 11;
 #endif
 }
 constexpr int kCamP = 65;  // LDS row pitch of the camera block (65: the four rows of a read in different banks)

@@ -46,6 +46,7 @@ VARIANTS = {
     "wait0vseq": (["CUSTMA_BWD_WAIT0", "CUSTMA_BWD_VSEQ"], BWD),
     "noslp": (["-fno-slp-vectorize"], BWD + ["stats.hip"]),  # no packed-fp32 pairing by the compiler
     "gather1": (["CUSTMA_BWD_GATHER1"], BWD),
+    "camlall": (["CUSTMA_BWD_CAMLDS_ALL"], BWD), "caml0": (["CUSTMA_BWD_CAMLDS=0"], BWD),
     # statistics tile: 32 x 32 pixels, 4 rows per thread is the default (profiles/r03/stats)
     "stats32x8": (["CUSTMA_STATS_TX=32", "CUSTMA_STATS_PR=8"], ["stats.hip"]),
     "stats16x8": (["CUSTMA_STATS_TX=16", "CUSTMA_STATS_PR=8"], ["stats.hip"]),

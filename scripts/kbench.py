@@ -15,6 +15,10 @@ CFGS = {
     # kernel sizes without a sweep instantiation (exact forward + generic fp64 backward)
     "c3_win_k17": dict(H=2048, W=2048, k=17, D=256, layout="window", dtype=torch.float16),
     "c3_win_k16": dict(H=2048, W=2048, k=16, D=256, layout="window", dtype=torch.float16),
+    # other sweep kernel sizes at C3 size
+    "c3_win_k5": dict(H=2048, W=2048, k=5, D=256, layout="window", dtype=torch.float16),
+    "c3_win_k9": dict(H=2048, W=2048, k=9, D=256, layout="window", dtype=torch.float16),
+    "c3_win_k13": dict(H=2048, W=2048, k=13, D=256, layout="window", dtype=torch.float16),
 }
 
 def warm(fn, secs=0.25):
