@@ -228,6 +228,30 @@ __device__ __forceinline__ void asm_ld_img8(uint32_t& pe0, uint32_t& pe1, uint32
             : "v"(vP0), "v"(vP1), "v"(vC0), "v"(vC1), "s"(dP), "s"(dC), "s"(sE), "s"(sL));
     }
 }
+// The projector half of asm_ld_img8 (the tile kernel's camera rows come from LDS: CPL).
+template <typename T>
+__device__ __forceinline__ void asm_ld_img4(uint32_t& pe0, uint32_t& pe1, uint32_t& pl0, uint32_t& pl1,
+                                            uint32_t vP0, uint32_t vP1, i32x4 dP, uint32_t sE, uint32_t sL) {
+    if constexpr (sizeof(T) == 4) {
+        asm volatile(
+            "s_nop 4\n\t"
+            "buffer_load_dword %0, %4, %6, %7 offen\n\t"
+            "buffer_load_dword %1, %5, %6, %7 offen\n\t"
+            "buffer_load_dword %2, %4, %6, %8 offen\n\t"
+            "buffer_load_dword %3, %5, %6, %8 offen"
+            : "=&v"(pe0), "=&v"(pe1), "=&v"(pl0), "=&v"(pl1)
+            : "v"(vP0), "v"(vP1), "s"(dP), "s"(sE), "s"(sL));
+    } else {
+        asm volatile(
+            "s_nop 4\n\t"
+            "buffer_load_ushort %0, %4, %6, %7 offen\n\t"
+            "buffer_load_ushort %1, %5, %6, %7 offen\n\t"
+            "buffer_load_ushort %2, %4, %6, %8 offen\n\t"
+            "buffer_load_ushort %3, %5, %6, %8 offen"
+            : "=&v"(pe0), "=&v"(pe1), "=&v"(pl0), "=&v"(pl1)
+            : "v"(vP0), "v"(vP1), "s"(dP), "s"(sE), "s"(sL));
+    }
+}
 __device__ __forceinline__ void asm_ld_stat6(double& m0, double& m1, uint32_t& q0, uint32_t& q1, double& ub,
                                              uint32_t& uq, uint32_t vM0, uint32_t vM1, uint32_t vQ0, uint32_t vQ1,
                                              uint32_t vUB, uint32_t vUQ, i32x4 dPB, i32x4 dPS, i32x4 dCB, i32x4 dCS,

@@ -71,12 +71,21 @@ constexpr bool kDppNop = CUSTMA_DPP_NOP != 0;
 // one of the 16 LDS rows (all D+1 diagonals of one camera pixel) for (best, second, first
 // index of best), AMX passes of 4 rows per wave, and writes them as one disparity partial.
 // AMX < 0: fused disparity with the soft-argmax sums (DispPartial::s0 / s1), -AMX passes.
-template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2, int AMX_ = 0>
+//
+// CPL (STAGED): the workgroup's camera rows h0 - R .. h1 + R - 1, columns u0 - R .. u0 - R + NX - 1
+// (every wave needs the same ones) are loaded once into LDS (camL, zero-padded) before the sweep,
+// instead of four 16-address loads per wave and step: those loads were most of the sweep's load
+// cost (C5: 9.80 -> 8.25 ms with every camera load out of range, profiles/r03/fwdabl).
+template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2, int AMX_ = 0,
+          bool CPL = false>
 __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
                                           const Stats& sc, const Stats& sp, float* __restrict__ out,
                                           int64_t u0, int64_t h0, int64_t h1, int64_t d0,
                                           double* rowE, double* rowL, double* sM, float* sQ, double* sR,
-                                          float* stage = nullptr, DispPartial part = DispPartial{}) {
+                                          float* stage = nullptr, DispPartial part = DispPartial{},
+                                          T* camL = nullptr) {
+    static_assert(!CPL || STAGED, "the camera preload is shared by the workgroup's waves");
+    typedef std::conditional_t<sizeof(T) == 2, unsigned short, uint32_t> RawT;  // raw image bits
     constexpr int AMX = AMX_ < 0 ? -AMX_ : AMX_;
     constexpr bool SOFT = AMX_ < 0;
     constexpr int R = K / 2, NX = TW + 2 * R;
@@ -102,6 +111,9 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
 #ifdef CUSTMA_ABL_NOSTATSMEM  // ablation (timing only): statistics loads out of range (no memory access)
     vM0 = vM1 = vQ0 = vQ1 = vUB = vUQ = OOB;
+#endif
+#ifdef CUSTMA_ABL_NOCAMMEM  // ablation (timing only): camera image-row and statistics loads out of range
+    vC0 = vC1 = vUB = vUQ = OOB;
 #endif
 #ifdef CUSTMA_ABL_NOIMGMEM  // ablation (timing only): image-row loads out of range
     vP0 = vP1 = vC0 = vC1 = OOB;
@@ -132,14 +144,28 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         uint32_t pe0, pe1, pl0, pl1, ce0, ce1, cl0, cl1, q0, q1, uq;
         double m0, m1, ub;
     };
-    constexpr int kLoads = 14;
+    constexpr int kLoads = CPL ? 10 : 14;
+    if constexpr (CPL) {
+        // camera rows h0 - R + i (i < h1 - h0 + 2R), columns u0 - R + j (j < NX), raw, 0 outside the image
+        typedef __attribute__((address_space(3))) RawT lds_t;
+        const RawT* cr = (const RawT*)cam;
+        const int nr = (int)(h1 - h0) + 2 * R;
+        for (int e = (int)threadIdx.x; e < nr * NX; e += (int)blockDim.x) {
+            const int64_t row = h0 - R + e / NX, c = u0 - R + e % NX;
+            ((lds_t*)camL)[e] = (row >= 0 && row < g.H && c >= 0 && c < g.W) ? cr[row * g.W + c] : (RawT)0;
+        }
+        __syncthreads();
+    }
     // step t adds image row t+R and removes row t-R-1 (rows from h0-R on were added, so the
     // first removal is at t = h0+1); statistics of row t (only for t in [h0, h1))
     auto load_step = [&](int64_t t, Stage& p) {
         const int ti = (int)t;
         const uint32_t sE = so_row(ti + R, rbT, true), sL = so_row(ti - R - 1, rbT, ti > h0i);
-        asm_ld_img8<T>(p.pe0, p.pe1, p.pl0, p.pl1, p.ce0, p.ce1, p.cl0, p.cl1, vP0, vP1, vC0, vC1, dProj, dCam, sE,
-                       sL);
+        if constexpr (CPL)
+            asm_ld_img4<T>(p.pe0, p.pe1, p.pl0, p.pl1, vP0, vP1, dProj, sE, sL);
+        else
+            asm_ld_img8<T>(p.pe0, p.pe1, p.pl0, p.pl1, p.ce0, p.ce1, p.cl0, p.cl1, vP0, vP1, vC0, vC1, dProj, dCam,
+                           sE, sL);
         const bool st = ti >= h0i && ti < h1i;
         asm_ld_stat6(p.m0, p.m1, p.q0, p.q1, p.ub, p.uq, vM0, vM1, vQ0, vQ1, vUB, vUQ, dPB, dPS, dCB, dCS,
                      so_row(ti, rb8, st), so_row(ti, rb4, st));
@@ -218,8 +244,20 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         sM[64 + l] = p.m1 * rk2;
         sQ[l] = __builtin_bit_cast(float, p.q0);
         sQ[64 + l] = __builtin_bit_cast(float, p.q1);
-        const double ca0 = raw_to_f64<T>(p.ce0), ca1 = raw_to_f64<T>(p.ce1);
-        const double cb0 = -raw_to_f64<T>(p.cl0), cb1 = -raw_to_f64<T>(p.cl1);
+        uint32_t ce0 = p.ce0, ce1 = p.ce1, cl0 = p.cl0, cl1 = p.cl1;
+        if constexpr (CPL) {
+            // the rows enter t + R and leave t - R - 1 (from t = h0 + 1 on) of the preloaded block
+            typedef __attribute__((address_space(3))) const RawT lds_ct;
+            const lds_ct* cr = (const lds_ct*)camL;
+            const int er = (int)(t - h0) + 2 * R, lr = (int)(t - h0) - 1;
+            const bool hi = 16 + r16 < NX, lv = t > h0;
+            ce0 = (uint32_t)cr[er * NX + r16];
+            ce1 = hi ? (uint32_t)cr[er * NX + 16 + r16] : 0u;
+            cl0 = lv ? (uint32_t)cr[lr * NX + r16] : 0u;
+            cl1 = lv && hi ? (uint32_t)cr[lr * NX + 16 + r16] : 0u;
+        }
+        const double ca0 = raw_to_f64<T>(ce0), ca1 = raw_to_f64<T>(ce1);
+        const double cb0 = -raw_to_f64<T>(cl0), cb1 = -raw_to_f64<T>(cl1);
         const double nb = -p.ub;                           // -(camera patch sum) of column r16
         const float uq = __builtin_bit_cast(float, p.uq);  // camera ex2 of column r16
 
@@ -503,7 +541,7 @@ __global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, cons
 constexpr int kTileP = CUSTMA_TILE_P;  // load pipeline depth (steps)
 constexpr int kWaveLds = (3 * kRowP + 64) * 8 + kRowP * 4;  // rowE, rowL, sM, sR (f64) + sQ (f32)
 
-template <int K, typename T, bool X4, int AMX = 0>
+template <int K, typename T, bool X4, int AMX = 0, bool CPL = false>
 __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __restrict__ cam,
                                                                  const T* __restrict__ proj, Geo g, Stats sc,
                                                                  Stats sp, float* __restrict__ out, WaveGrid wg,
@@ -517,6 +555,7 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     double* sR = sM + kRowP;
     float* sQ = (float*)(sR + 64);
     float* stage = (float*)((char*)lds_t + wg.nChunk * kWaveLds);
+    T* camL = (T*)(stage + 2 * TW * g.DO);  // CPL: the camera block after the two stage buffers
     const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
     const int wt = (int)(bid % wg.nTile);
     const int band = (int)(bid / wg.nTile);
@@ -528,14 +567,30 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
     constexpr int kTP = X4 ? kTileP : 2;  // deeper pipelines only with the 16-byte stores (vmcnt range)
     if (!wg.rem)
-        wave_body<K, T, false, false, true, S0, kTP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
-                                                             sQ, sR, stage, part);
+        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL,
+                                                                  sM, sQ, sR, stage, part, camL);
     else if (w == wg.nChunk - 1)
-        wave_body<K, T, false, true, true, S1, kTP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
-                                                            sQ, sR, stage, part);
+        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL,
+                                                                 sM, sQ, sR, stage, part, camL);
     else
-        wave_body<K, T, false, false, true, S1, kTP, AMX>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL, sM,
-                                                             sQ, sR, stage, part);
+        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL,
+                                                                  sM, sQ, sR, stage, part, camL);
+}
+
+// CPL: fp16 images, when the camera block keeps the tile kernel at three workgroups per CU (LDS
+// <= 160 KiB / 3); CUSTMA_FWD_CPL=0 turns it off (benchmarking only).  Volume form: C5 9.81 -> 9.15 ms,
+// C3 unchanged (profiles/r03/cpl); the fused disparity keeps its per-step camera loads.
+template <int K, typename T>
+size_t cpl_bytes(const WaveGrid& wg) {
+    constexpr int R = K / 2, NX = TW + 2 * R;
+    return ((size_t)(wg.TH + 2 * R) * NX * sizeof(T) + 15) & ~(size_t)15;
+}
+template <int K, typename T>
+bool cpl_ok(const Geo& g, const WaveGrid& wg, size_t lds) {
+    (void)g;
+    const char* e = getenv("CUSTMA_FWD_CPL");
+    if (e && atoi(e) == 0) return false;
+    return sizeof(T) == 2 && lds + cpl_bytes<K, T>(wg) <= 163840 / 3;
 }
 
 template <int K, typename T>
@@ -546,13 +601,19 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
     prof_begin(PROF_FWD, s);
     if (tile) {
         const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
-        const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
+        size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
+        const bool cpl = cpl_ok<K, T>(g, wg, lds);
+        if (cpl) lds += cpl_bytes<K, T>(wg);
         // 16-byte stores when every block base is 16-byte aligned: out aligned and
         // ((t - h_lo) WO + u0) DO = 0 mod 4 for all t (u0 = 0 mod 16)
         const char* e4 = getenv("CUSTMA_FWD_X4");  // benchmarking only: 0 = dword stores
         const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0) && !(e4 && atoi(e4) == 0);
         const dim3 blk(64 * wg.nChunk);
-        if (x4)
+        if (x4 && cpl) {
+            if constexpr (sizeof(T) == 2)
+                hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, true>), dim3((unsigned)blocks), blk, lds, s, cam, proj, g,
+                                   sc, sp, out, wg, DispPartial{});
+        } else if (x4)
             hipLaunchKernelGGL((k_fwd_tile<K, T, true>), dim3((unsigned)blocks), blk, lds, s, cam, proj, g, sc, sp,
                                out, wg, DispPartial{});
         else
@@ -572,12 +633,22 @@ template <int K, typename T>
 hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, DispPartial part, hipStream_t s) {
     const WaveGrid wg = wave_grid(g);
     const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
-    const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
+    size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
+    // the camera preload measured slower here (C5 9.69 -> 9.99 ms, C3 1.15 -> 1.18 ms): opt-in only
+    const char* ec = getenv("CUSTMA_DISP_CPL");
+    const bool cpl = ec && atoi(ec) != 0 && cpl_ok<K, T>(g, wg, lds);
+    if (cpl) lds += cpl_bytes<K, T>(wg);
     prof_begin(PROF_FWD, s);
     const int passes = wg.nChunk == 4 ? 1 : wg.nChunk >= 2 ? 2 : 4;  // 16 rows over the waves, 4 per pass
     auto go = [&](auto amx) {
-        hipLaunchKernelGGL((k_fwd_tile<K, T, false, decltype(amx)::value>), dim3((unsigned)blocks),
-                           dim3(64 * wg.nChunk), lds, s, cam, proj, g, sc, sp, nullptr, wg, part);
+        if (cpl) {
+            if constexpr (sizeof(T) == 2)
+                hipLaunchKernelGGL((k_fwd_tile<K, T, false, decltype(amx)::value, true>), dim3((unsigned)blocks),
+                                   dim3(64 * wg.nChunk), lds, s, cam, proj, g, sc, sp, nullptr, wg, part);
+        } else {
+            hipLaunchKernelGGL((k_fwd_tile<K, T, false, decltype(amx)::value>), dim3((unsigned)blocks),
+                               dim3(64 * wg.nChunk), lds, s, cam, proj, g, sc, sp, nullptr, wg, part);
+        }
     };
     const bool soft = part.s0 != nullptr;  // soft-argmax sums requested
     if (passes == 1) soft ? go(std::integral_constant<int, -1>{}) : go(std::integral_constant<int, 1>{});

@@ -17,7 +17,7 @@ VARIANTS = {
     "storeonly": (["CUSTMA_ABL_NOUPDATE", "CUSTMA_ABL_NOOUT"], FWD),
     "nowait": (["CUSTMA_ABL_NOWAIT"], FWD),
     "nostatsmem": (["CUSTMA_ABL_NOSTATSMEM"], FWD), "noimgmem": (["CUSTMA_ABL_NOIMGMEM"], FWD),
-    "noldmem": (["CUSTMA_ABL_NOSTATSMEM", "CUSTMA_ABL_NOIMGMEM"], FWD), "stats7": (["CUSTMA_ABL_STATS7"], FWD),
+    "noldmem": (["CUSTMA_ABL_NOSTATSMEM", "CUSTMA_ABL_NOIMGMEM"], FWD), "nocammem": (["CUSTMA_ABL_NOCAMMEM"], FWD), "stats7": (["CUSTMA_ABL_STATS7"], FWD),
     "early": (["CUSTMA_TILE_EARLY"], FWD), "tileP3": (["CUSTMA_TILE_P=3"], FWD),
     # volume-store cache policy (gfx950 aux bits: 1 sc0, 2 nt, 16 sc1)
     "st_plain": (["CUSTMA_STORE_AUX=0"], FWD), "st_sc1": (["CUSTMA_STORE_AUX=16"], FWD),
