@@ -345,7 +345,7 @@ def main():
 
     import custereomatching_amd as cm
     from custereomatching_amd import _lib
-    from custereomatching_amd.rowband import stereo_matching_rowband
+    from custereomatching_amd import rowband
 
     wl = WORKLOADS[args.workload]
     H, W, k, D, layout = wl["H"], wl["W"], wl["k"], wl["D"], wl["layout"]
@@ -353,10 +353,12 @@ def main():
     cam.requires_grad_(True)
     proj.requires_grad_(True)
     global_H = H if wl["scaling"] == "strong" else H * world
+    # the row-band group (halo sizes, the collective band check) once for the whole run
+    rbg = rowband.RowBandGroup(k, None, n=cam.shape[0], H=global_H, device=dev) if distributed else None
 
     def op():
         if distributed:
-            return stereo_matching_rowband(cam, proj, D, k, layout, args.precision, H=global_H)
+            return rowband.stereo_matching_rowband(cam, proj, D, k, layout, args.precision, rbg=rbg)
         return cm.stereo_matching(cam, proj, D, k, layout, args.precision)
 
     def step():
@@ -374,6 +376,8 @@ def main():
     # HIP events around the two sweep kernels of every op in the timed region (recorded by the
     # library on the op's stream; custma_profile_*), for the roofline figures
     _lib.profile_enable(True)
+    if distributed:
+        rowband.enable_timing(args.dist_backend == "nccl")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -385,6 +389,17 @@ def main():
     fwd_kms, n_fk = _lib.profile_mean_ms(_lib.PROF_FWD)
     bwd_kms, n_bk = _lib.profile_mean_ms(_lib.PROF_BWD)
     _lib.profile_enable(False)
+    per_rank = None
+    if distributed:
+        # per rank: sweep kernel times (HIP events; the forward's interior + edge launches are
+        # separate launches) and the exchange times the op's stream waited for (rowband timing)
+        mine = {"rank": rank, "rows": int(cam.shape[0]), "fwd_sweep_launch_ms": round(fwd_kms, 4),
+                "fwd_sweep_launches_per_step": round(n_fk / max(1, args.steps), 2),
+                "bwd_sweep_launch_ms": round(bwd_kms, 4), "step_ms_local": round(elapsed / args.steps * 1e3, 4)}
+        mine.update(rowband.timing_summary() if args.dist_backend == "nccl" else {})
+        rowband.enable_timing(False)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     rows = cam.shape[0]
     WO, DO = (W, W) if layout == "full" else (W - D, D + 1)
     nvox_rank = rows * WO * DO
@@ -418,15 +433,19 @@ def main():
     bwd_bytes = nvox_rank * 4 + img + 2 * cam.numel() * 4
     bwd_design = bwd_bytes + nvox_rank * 4
     fwd_name = fwd_kernel_name(layout, W, D)
+    # at N > 1 the forward runs as an interior launch + two edge launches per step (rowband):
+    # its bytes are per step, so its time is the per-step sum of those launches
+    fwd_step_ms = fwd_kms * n_fk / max(1, args.steps)
     kern = {
-        fwd_name: {"avg_launch_ms": round(fwd_kms, 4), "launches": n_fk, "algorithmic_bytes": fwd_bytes,
-                   "achieved_GBps": round(fwd_bytes / (fwd_kms * 1e-3) / 1e9, 1) if fwd_kms else None},
+        fwd_name: {"avg_launch_ms": round(fwd_kms, 4), "launches": n_fk, "ms_per_step": round(fwd_step_ms, 4),
+                   "algorithmic_bytes": fwd_bytes,
+                   "achieved_GBps": round(fwd_bytes / (fwd_step_ms * 1e-3) / 1e9, 1) if fwd_kms else None},
         "k_bwd_coop": {"avg_launch_ms": round(bwd_kms, 4), "launches": n_bk, "algorithmic_bytes": bwd_bytes,
                        "design_bytes": bwd_design,
                        "achieved_GBps": round(bwd_bytes / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None,
                        "design_GBps": round(bwd_design / (bwd_kms * 1e-3) / 1e9, 1) if bwd_kms else None},
     }
-    dom = "k_bwd_coop" if bwd_kms >= fwd_kms else fwd_name
+    dom = "k_bwd_coop" if bwd_kms >= fwd_step_ms else fwd_name
     dk = kern[dom]
     achieved = dk["achieved_GBps"] or 0.0
     result = {
@@ -468,6 +487,8 @@ def main():
         },
         "kernels": kern,
     }
+    if per_rank is not None:
+        result["per_rank"] = per_rank
     del g
     cam.grad = proj.grad = None
     torch.cuda.empty_cache()

@@ -53,32 +53,19 @@ namespace custma {
 
 namespace {
 
-#ifndef CUSTMA_BWD_ROWS
-#define CUSTMA_BWD_ROWS 16
-#endif
-constexpr int TRB = CUSTMA_BWD_ROWS;  // own rows per unit (workgroup)
+// own rows per unit (workgroup); 32-row units re-read fewer halo rows but one 8-wave workgroup per
+// CU ran slower (C5 44.3 vs 39.1 ms, round 2)
+constexpr int TRB = 16;
 constexpr int NLB = 64;   // diagonals per wave
 constexpr int NTYPE = 6;  // partial types: T1c, Am, B (camera) | T1p, Ac, Bp (projector)
-#ifndef CUSTMA_BWD_SEG
-#define CUSTMA_BWD_SEG 512  // 128 -> 512: C5 window backward 28.9 -> 27.6-28.0 ms, C2 full 3.57 -> 3.38 ms (profiles/r03/seg_ab.txt)
-#endif
+// 128 -> 512 columns: C5 window backward 28.9 -> 27.6-28.0 ms, C2 full 3.57 -> 3.38 ms (profiles/r03/seg_ab.txt)
 // most pixel columns per unit; a unit sweeps its segment + 2 r columns, so the 2 r halo steps are
 // 2 r / segment of redundant work.  A chunk's columns are cut into equal segments of at most kSeg
 // (chunk_geo; an unequal last segment left the last round of units half idle: C3 has 4 segments
 // of 451 columns, not 3 of 512 + 1 of 266).  Every segment holds >= 64 + 2 r columns whenever a
 // chunk has two or more, so segments s and s + 2 never overlap (slot parity).
-constexpr int kSeg = CUSTMA_BWD_SEG;
+constexpr int kSeg = 512;
 constexpr uint32_t kOOB = 0x80000000u;
-#ifndef CUSTMA_BWD_PF
-#define CUSTMA_BWD_PF 2
-#endif
-constexpr int kPF = CUSTMA_BWD_PF;  // rows of loads in flight ahead of the row being computed
-#ifndef CUSTMA_BWD_VAUX
-#define CUSTMA_BWD_VAUX 0  // cache-policy bits of the gradient / volume loads (gfx950: 1 sc0, 2 nt, 16 sc1)
-#endif
-__device__ __forceinline__ float ld_vol(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t so) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, so, CUSTMA_BWD_VAUX));
-}
 
 // Chunk geometry (host and device): diagonals [d0, d0+64); camera columns that carry
 // a valid voxel for some lane: [wlo, whi); pixel columns whose box touches one:
@@ -177,41 +164,24 @@ __device__ __forceinline__ int chunk_of_rank(int r, int n, int jc) {
 // V of its own rows and slides them horizontally with a k-deep LDS ring of its own V
 // (HV += V(w) - V(w-k)).  So the leaving column is never re-read, no halo row is loaded
 // twice within a unit, and the leaving column's Y is not needed at all.  Taller units
-// (CUSTMA_BWD_ROWS = 32: 8 waves) re-read fewer halo rows of the gradient: (TRB + 2r) / TRB
-// gradient reads per voxel.
+// (32 rows: 8 waves) would re-read fewer halo rows of the gradient: (TRB + 2r) / TRB gradient
+// reads per voxel.
 constexpr int TRW = 4;           // own rows per wave
 constexpr int NWC = TRB / TRW;   // waves per cooperative workgroup
 #ifndef CUSTMA_BWD_DEPTH
-#define CUSTMA_BWD_DEPTH 1  // 2 measured no faster (C2 full 5.37 vs 5.19 ms): latency is not the limit
+#define CUSTMA_BWD_DEPTH 1
 #endif
 constexpr int BDP = CUSTMA_BWD_DEPTH;  // steps of loads in flight (1 or 2)
-#ifndef CUSTMA_BWD_SLIDE
-#define CUSTMA_BWD_SLIDE 1
-#endif
-// Sliding projector-side columns: the per-voxel projector values Y, mp', p' of a lane at
-// column w + dl are the next lane's values of the previous step, so they move down one
-// lane per step (DPP wave_shl:1) and only lane 63 takes a new column, read from a register
-// loaded once per 64 steps -- instead of a 64-lane load of each per step (those image rows
-// do not stay in L2 beside the gradient stream: ~half of the kernel's L2 misses).
-constexpr bool SLIDE = CUSTMA_BWD_SLIDE;
-// steps per flush (small buffers: 3 workgroups per CU at k = 9); a multiple of BDP + 1, so
-// every flush block starts on load buffer 0
-// 16 steps per flush (all 64 lanes store: 4 rows x 16 steps) where the LDS allows it: C5 window
-// backward op 27.7 -> 26.7 ms, C3 3.26 -> 3.19 ms (profiles/r03/win_fbc_ab.txt).  k <= 9 keeps 8, so
-// its 3 workgroups per CU still fit.
-#ifdef CUSTMA_BWD_FBC
+// The per-voxel projector values Y, mp', p' of a lane at column w + dl are the next lane's
+// values of the previous step, so they slide down one lane per step (DPP wave_shl:1) and only
+// lane 63 takes a new column, read from a register loaded once per 64 steps -- instead of a
+// 64-lane load of each per step (those image rows do not stay in L2 beside the gradient
+// stream: ~half of the kernel's L2 misses).
+// Steps per flush, a multiple of BDP + 1 (every flush block starts on load buffer 0).  16 (all 64
+// lanes store: 4 rows x 16 steps) where the LDS allows it: C5 window backward op 27.7 -> 26.7 ms,
+// C3 3.26 -> 3.19 ms (profiles/r03/win_fbc_ab.txt); k <= 9 keeps 8, so its 3 workgroups per CU fit.
 template <int K>
-constexpr int fbc_for() { return CUSTMA_BWD_FBC; }
-#else
-template <int K>
-constexpr int fbc_for() { return BDP == 2 ? 6 : K >= 11 ? 16 : 8; }
-#endif
-// A rows of the unit: double-buffered (one barrier per step) or single (a second barrier
-// before the next step's writes; 6.5 KB less LDS at k = 11)
-#ifndef CUSTMA_BWD_ABUF
-#define CUSTMA_BWD_ABUF 2
-#endif
-constexpr int NAB = CUSTMA_BWD_ABUF;
+constexpr int fbc_for() { return BDP == 2 ? (K >= 11 ? 12 : 6) : K >= 11 ? 16 : 8; }
 
 // Finish 3 registers (each already summed over the 4 lanes {l, l+16, l+32, l+48}, one
 // value per 16-lane row): afterwards every lane holds the full 64-lane sum of one of the 12.
@@ -246,13 +216,7 @@ __device__ __forceinline__ F tree_sum(const F* c) {
 // (+54 %), k = 15, 17 are there already.
 template <int K>
 constexpr bool cam_lds_for() {
-#ifdef CUSTMA_BWD_CAMLDS_ALL  // benchmarking: every kernel size (k = 7, 9, 13 then lose a workgroup per CU)
-    return true;
-#elif defined(CUSTMA_BWD_CAMLDS)
-    return CUSTMA_BWD_CAMLDS != 0 && K <= 11;
-#else
     return K <= 11;
-#endif
 }
 constexpr int kCamP = 65;  // LDS row pitch of the camera block (65: the four rows of a read in different banks)
 
@@ -335,7 +299,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         return make_rsrc(a.part + ((size_t)t * a.S + slot) * plane + (size_t)(y0 + yw) * g.W, prow_bytes);
     };
     // loads per issue() (asm_ld2s / asm_ld1s / asm_ld4), per thread
-    constexpr int NLD = (SLIDE ? TRW * 2 + (HPW > 0 ? HPW : 1) : TRW * 5 + (HPW > 0 ? HPW : 1) * 2) + (CAML ? 0 : 4);
+    constexpr int NLD = TRW * 2 + (HPW > 0 ? HPW : 1) + (CAML ? 0 : 4);
     auto flush = [&](int wfirst, int nsteps) {
         if constexpr (BDP == 2) asm_vmcnt<NLD>();  // all but the newest issue
         int ln = lane;
@@ -409,7 +373,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     struct Ld {
         // xo / mc / cx: lane l holds own row l & 3 (row-replicated per 16 lanes, read back with
         // DPP row_newbcast); xh: lane l holds the wave's halo row l & 3
-        uint32_t ge[TRW], cv[TRW], Ye[TRW], mp[TRW], pq[TRW], hg[HP], hY[HP], xo, xh, mc, cx;
+        uint32_t ge[TRW], cv[TRW], hg[HP], xo, xh, mc, cx;
     };
     // NOP: open each load group with `s_nop 4` (VALU SGPR write -> VMEM read); the in-loop
     // issues go without -- their descriptors / soffsets are loop constants, written (by
@@ -440,35 +404,16 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             return;
         }
         const bool ve = w >= lwlo && w < lwhi;
-#ifdef CUSTMA_ABL_BWD_NOMEM  // ablation (timing only): no gradient / volume traffic
-        const uint32_t oGe = kOOB + 0 * ve;
-#else
         const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
-#endif
-        const uint32_t oYe = col_off_a(w + dl, kY), oMe = col_off_a(w + dl, kMp), oPq = col_off_a(xb + dl, kP);
-        if constexpr (SLIDE) {
 #pragma unroll
-            for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
+        for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
 #pragma unroll
-            for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], wv + NWC * i < NH ? oGe : kOOB, dG, sVh[i]);
-        } else {
-#pragma unroll
-            for (int m = 0; m < TRW; ++m) {
-                asm_ld2s<NOP>(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
-                asm_ld2s<NOP>(b.Ye[m], b.mp[m], oYe, oMe, dPr, dPr, sIo[m], sIo[m]);
-                asm_ld1s<NOP>(b.pq[m], oPq, dPr, sIo[m]);
-            }
-#pragma unroll
-            for (int i = 0; i < HP; ++i) {
-                const bool ok = wv + NWC * i < NH;
-                asm_ld2s<NOP>(b.hg[i], b.hY[i], ok ? oGe : kOOB, ok ? oYe : kOOB, dG, dPr, sVh[i], sIh[i]);
-            }
-        }
+        for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], wv + NWC * i < NH ? oGe : kOOB, dG, sVh[i]);
         if constexpr (!CAML)
         asm_ld4<NOP>(b.xo, b.xh, b.mc, b.cx, img_off_a(orow_l, w, kX), hrow_l >= 0 ? img_off_a(hrow_l, w, kX) : kOOB,
                 img_off_a(orow_l, w, kMc), img_off_a(orow_l, xb, kC), dPr, dPr, dPr);
     };
-    // SLIDE: the current step's projector-side columns (lane l: column w + dl, p': w - R + dl)
+    // the current step's projector-side columns (lane l: column w + dl, p': w - R + dl)
     // and the once-per-64-steps column block whose lane i feeds lane 63 at step w0 + 1 + 64k + i
     // sc[3m + {0, 1, 2}] = Y, mp', p' of own row m; bc the same for the block
     uint32_t sc[3 * TRW], shY[HP], bc[3 * TRW], bhY[HP];
@@ -516,15 +461,11 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
             asm_tie(b.ge[m]); asm_tie(b.cv[m]);
-            if constexpr (!SLIDE) { asm_tie(b.Ye[m]); asm_tie(b.mp[m]); asm_tie(b.pq[m]); }
         }
 #pragma unroll
-        for (int i = 0; i < HP; ++i) {
-            asm_tie(b.hg[i]);
-            if constexpr (!SLIDE) asm_tie(b.hY[i]);
-        }
+        for (int i = 0; i < HP; ++i) asm_tie(b.hg[i]);
         asm_tie(b.xo); asm_tie(b.xh); asm_tie(b.mc); asm_tie(b.cx);
-        if constexpr (SLIDE || CAML) tie_cols();
+        tie_cols();
     };
     auto F = [](uint32_t u) { return __builtin_bit_cast(float, u); };
 
@@ -550,28 +491,25 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     };
     auto step = [&](Ld& cur, Ld& nxt, int w, int s, bool flushed) {
         if constexpr (BDP == 2) {
-            // SLIDE: a column block issued at s = 0 (after the flush's stores) feeds step 1
-            if (!flushed || s >= 2 || (SLIDE && s == 1)) asm_vmcnt<NL>();
+            // a column block issued at s = 0 (after the flush's stores) feeds step 1
+            if (!flushed || s >= 1) asm_vmcnt<NL>();
             else if (s == 1) asm_vmcnt<NL + SF>();
         } else {
-#ifdef CUSTMA_BWD_WAIT0
-            asm_vmcnt<0>();
-#else
-            // the step's loads, not the flush's SF stores issued after them (a store's completion
-            // is not needed here; vmcnt counts loads and stores in issue order)
+            // the step's loads, not the flush's SF stores issued after them: a store's completion
+            // is not needed here, and on gfx950 `s_waitcnt vmcnt(N)` counts loads, stores, atomics
+            // and LDS-DMA together in issue order, so vmcnt(SF) waits for every load issued before
+            // those SF stores (MI355X_MICROARCH.md, the vmcnt paragraph after the cycle constants;
+            // LLVM's own waitcnt pass does not assume this ordering, hence the hand-counted wait)
             if (flushed && s == 0) asm_vmcnt<SF>();
             else asm_vmcnt<0>();
-#endif
         }
         tie(cur);
-        if constexpr (SLIDE) {
-            if (w > w0) {  // move the columns down one lane; lane 63 takes column w + 63 (+ offset)
-                slide_rows<HP>(sc, bc, shY, bhY, lane63);
-            }
-            // the block for steps w + 1 .. w + 64 (lane i -> step w + 1 + i): columns w + 64 + i (+ offset);
-            // issued after this step's reads of the previous block
-            if (((w - w0) & 63) == 0) load_cols(bc, bhY, w + 64);
+        if (w > w0) {  // move the columns down one lane; lane 63 takes column w + 63 (+ offset)
+            slide_rows<HP>(sc, bc, shY, bhY, lane63);
         }
+        // the block for steps w + 1 .. w + 64 (lane i -> step w + 1 + i): columns w + 64 + i (+ offset);
+        // issued after this step's reads of the previous block
+        if (((w - w0) & 63) == 0) load_cols(bc, bhY, w + 64);
         uint32_t cxo_r = cur.xo, cxh_r = cur.xh, cmc_r = cur.mc, ccx_r = cur.cx;
         if constexpr (CAML) {
             typedef __attribute__((address_space(3))) float lds_f;
@@ -589,7 +527,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             cxh_r = __builtin_bit_cast(uint32_t, cl[(12 + (q < HP ? q : HP - 1)) * kCamP + cc]);
         }
         issue(w + BDP, nxt, std::false_type{});  // past the segment's end: harmless, drained before the wave ends
-        float* Acur = Abuf + (NAB == 2 ? ((w - w0) & 1) * (NY * 64) : 0);
+        float* Acur = Abuf + ((w - w0) & 1) * (NY * 64);  // double-buffered: one barrier per step
         // this wave's ring slot of the step (V of its rows K steps ago): wave-private, so read
         // ahead of the barrier
         float rsv[TRW];
@@ -607,16 +545,15 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         // ---- own rows: A, and the per-voxel terms (unit rows R + yw .. R + yw + 3); the
         // row's camera values come from quad slot m of the row-replicated registers ----
         float amv[TRW], bv[TRW];
-        if constexpr (NAB == 1) __syncthreads();  // every wave has read the previous step's A rows
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
             const int y = R + yw + m;
-            const float Xf = rbc<m>(F(cxo_r)), Ye = F(SLIDE ? sc[3 * m] : cur.Ye[m]);
+            const float Xf = rbc<m>(F(cxo_r)), Ye = F(sc[3 * m]);
             const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, Ye, kEps));
             const float Ae = F(cur.ge[m]) * rSe;
             Acur[y * 64 + lane] = Ae;
             const float V = Ae * F(cur.cv[m]) * rSe;
-            amv[m] = Ae * F(SLIDE ? sc[3 * m + 1] : cur.mp[m]);
+            amv[m] = Ae * F(sc[3 * m + 1]);
             bv[m] = V * Ye;
             P[1][m] = shl1_add(P[1][m], Ae * rbc<m>(mco));
             P[2][m] = shl1_add(P[2][m], (V * af) * Xf);
@@ -627,7 +564,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             if (q < NH) {
                 const int y = halo_row(q);
                 Acur[y * 64 + lane] = F(cur.hg[i]) * __builtin_amdgcn_rsqf(
-                                                         __builtin_fmaf(rbc<i>(F(cxh_r)), F(SLIDE ? shY[i] : cur.hY[i]), kEps));
+                                                         __builtin_fmaf(rbc<i>(F(cxh_r)), F(shY[i]), kEps));
             }
         });
         if (s > 0) reduce_to(s - 1);
@@ -636,20 +573,14 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         float col[TRW + 2 * R];
 #pragma unroll
         for (int y = 0; y < TRW + 2 * R; ++y) col[y] = Acur[(yw + y) * 64 + lane];
-#ifdef CUSTMA_BWD_VSEQ
-        float v = 0.f;
-#pragma unroll
-        for (int y = 0; y <= 2 * R; ++y) v += col[y];
-#else
         float v = tree_sum<2 * R + 1>(col);  // a pairwise tree: depth log2(k) instead of a k-long chain
-#endif
         float t1v[TRW];
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
             if (m > 0) v = (v + col[m + 2 * R]) - col[m - 1];
             HV[m] += v - rsv[m];
             ring[(sidx * TRW + m) * 64 + lane] = v;
-            t1v[m] = (F(SLIDE ? sc[3 * m + 2] : cur.pq[m]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
+            t1v[m] = (F(sc[3 * m + 2]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
             P[0][m] = shl1_add(P[0][m], rbc<m>(cxo) * HV[m]);
         });
         sidx = sidx + 1 == K ? 0 : sidx + 1;
@@ -662,7 +593,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     };
 
     Ld L[BDP + 1];
-    if constexpr (SLIDE) load_cols(sc, shY, w0);  // the first step's columns, all lanes
+    load_cols(sc, shY, w0);  // the first step's columns, all lanes
     load_cam(w0);  // CAML: the first block (written to LDS at step w0)
     issue(w0, L[0], std::true_type{});
     if constexpr (BDP == 2) issue(w0 + 1, L[1], std::true_type{});
@@ -692,7 +623,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     asm_vmcnt<0>();
 #pragma unroll
     for (int i = 0; i <= BDP; ++i) tie(L[i]);
-    if constexpr (SLIDE || CAML) tie_cols();
+    tie_cols();
     // ---- final projector state: lane l holds column (wend - 1) + off + d0 + l
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
@@ -788,6 +719,9 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
     // horizontal box over the lanes x - R .. x + R of a product row (own lanes)
     auto hbox = [&](double v) {
         xp[lane] = v;
+        // other lanes' slots are read next: keep those loads after this store (a wave's LDS
+        // accesses execute in program order; this pins the compiler's order)
+        __builtin_amdgcn_wave_barrier();
         double c[2 * R + 1];
 #pragma unroll
         for (int j = 0; j <= 2 * R; ++j) c[j] = xp[own ? lane - R + j : 0];
@@ -844,6 +778,7 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
         const int y = h - R;
         if (y >= y0) {
             xs[lane] = VS;
+            __builtin_amdgcn_wave_barrier();  // as in hbox: the cross-lane reads stay after the store
             float c[2 * R + 1];
 #pragma unroll
             for (int j = 0; j <= 2 * R; ++j) c[j] = xs[own ? lane - R + j : 0];
@@ -864,13 +799,8 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
     }
 }
 
-#ifdef CUSTMA_BWD_WPE
-#define CUSTMA_BWD_OCC __attribute__((amdgpu_waves_per_eu(CUSTMA_BWD_WPE)))
-#else
-#define CUSTMA_BWD_OCC
-#endif
 template <int K, bool WIN>
-__global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, BwdArgs a) {
+__global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
     // XCD x owns row groups [x nRGx, (x+1) nRGx) (their halo rows are read on one XCD).
     // A wave's 256-byte gradient / volume row segment spans three 128-byte lines whose outer
     // parts the neighbouring diagonal chunk's workgroup reads at the same step; the order
@@ -902,7 +832,7 @@ __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, Bwd
     }
     if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
     constexpr int NY = TRB + 2 * (K / 2);
-    __shared__ __attribute__((aligned(16))) float Abuf[NAB * NY * 64];
+    __shared__ __attribute__((aligned(16))) float Abuf[2 * NY * 64];
     __shared__ __attribute__((aligned(16))) float ring[NWC * K * TRW * 64];
     constexpr int FBC = fbc_for<K>();
     __shared__ __attribute__((aligned(16))) float cbuf[NWC][FBC][12];
@@ -918,9 +848,8 @@ __global__ __launch_bounds__(64 * NWC) CUSTMA_BWD_OCC void k_bwd_coop(Geo g, Bwd
 // cover layout: [3][W] counts, then [3][W][S] slot indices (uint16).
 // cover_column counts every (chunk, segment) whose written range holds column x and stores the
 // first S slot indices into `list` (when given).  plan_bwd's S bounds the count by construction
-// (2 x the max chunk overlap, <= 2 segments per chunk); the host re-checks that for every column
-// (cover_fits), and the device marks an over-full column with count -1, which k_bwd_gather turns
-// into NaN gradients -- never a silently dropped slot.
+// (2 x the max chunk overlap, <= 2 segments per chunk); the device marks an over-full column with
+// count -1, which k_bwd_gather turns into NaN gradients -- never a silently dropped slot.
 __host__ __device__ inline int cover_column(const Geo& g, int64_t dlo, int nChunk, int S, int Sj, int64_t x, int cls,
                                             unsigned short* list) {
     const int t = cls == 0 ? 0 : cls == 1 ? 3 : 4;
@@ -995,18 +924,14 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
     return s;
 }
 
-// Per-pixel sums (k_bwd_gather -> k_bwd_combine2): fp64 sums of the fp32 chunk partials, stored as
+// Per-pixel sums (k_bwd_gather -> k_bwd_combine3): fp64 sums of the fp32 chunk partials, stored as
 // fp32 (one more rounding of values that are sums of fp32 partials already; the box filters and the
-// final combination stay fp64).  CUSTMA_BWD_ACC64: fp64 storage (benchmarking / checking only).
-#ifdef CUSTMA_BWD_ACC64
-typedef double acc_t;
-#else
+// final combination stay fp64).
 typedef float acc_t;
-#endif
 
-// Sum the partial slots per pixel; out ([2 sides][3][H][W]): T1, Z = Am|Ac - m' B|Bp, B|Bp (k_bwd_combine3;
-// CUSTMA_BWD_GATHER1: T1, Am|Ac, B|Bp for k_bwd_combine2, the round-2 pair)
-// forms m' B as it loads its tile -- the same product, one fp64 array less through HBM).
+// Sum the partial slots per pixel; out ([2 sides][3][H][W]): T1, Z = Am|Ac - m' B|Bp, B|Bp (k_bwd_combine3
+// forms no patch sums: the gather forms m' B as it loads its tile -- the same product, one fp64 array less
+// through HBM).
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, acc_t* acc, const float* remT,
                                                     const float* remT1) {
@@ -1021,83 +946,14 @@ __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, acc_t* acc
 #pragma unroll
         for (int q = 0; q < 3; ++q) s[q] = gather_sum(g, a, remT, remT1, side, q, y, x, p);
     }
-#ifndef CUSTMA_BWD_GATHER1
     // Z = A - m' B (m' = box / k^2 - shift, the pixel's shifted patch mean): k_bwd_combine3 then
     // needs two box filters, Box[Z] = Box[A] - Box[m' B], and no patch sums
     const double* box = side == 0 ? a.sc.box : a.sp.box;
     s[1] -= s[2] * (box[p] / (double)(g.k * g.k) - (double)a.shift[side]);
-#endif
     acc_t* o = acc + (size_t)side * 3 * plane;
     o[p] = (acc_t)s[0];
     o[plane + p] = (acc_t)s[1];
     o[2 * plane + p] = (acc_t)s[2];
-}
-
-// grad(y,x) = T1 - Box[A] - img'(y,x) Box[B] + Box[m' B]   (one side per blockIdx.z)
-template <typename T>
-__global__ __launch_bounds__(256) void k_bwd_combine2(Geo g, const T* __restrict__ cam, const T* __restrict__ proj,
-                                                      const float* __restrict__ shift, const acc_t* __restrict__ acc,
-                                                      Stats sc, Stats sp, float* __restrict__ dcam,
-                                                      float* __restrict__ dproj) {
-    constexpr int TS = 16;
-    extern __shared__ __attribute__((aligned(16))) double tl[];
-    const int side = blockIdx.z;
-    float* out = side == 0 ? dcam : dproj;
-    if (!out) return;
-    const T* img = side == 0 ? cam : proj;
-    const int64_t plane = g.H * g.W;
-    const acc_t* T1 = acc + (size_t)side * 3 * plane;
-    const acc_t* Aa = T1 + plane;
-    const acc_t* Bb = Aa + plane;
-    const double* box = side == 0 ? sc.box : sp.box;
-    const double sh = (double)shift[side], rk2 = (double)(g.k * g.k);
-    const int r = g.r, L = TS + 2 * r;
-    double* tA = tl;
-    double* tB = tA + L * L;
-    double* tM = tB + L * L;
-    const int64_t y0 = (int64_t)blockIdx.y * TS, x0 = (int64_t)blockIdx.x * TS;
-    for (int e = threadIdx.x; e < L * L; e += 256) {
-        const int64_t y = y0 + e / L - r, x = x0 + e % L - r;
-        const bool ok = y >= 0 && y < g.H && x >= 0 && x < g.W;
-        const int64_t q = y * g.W + x;
-        const double b = ok ? Bb[q] : 0.0;
-        tA[e] = ok ? Aa[q] : 0.0;
-        tB[e] = b;
-        tM[e] = ok ? b * (box[q] / rk2 - sh) : 0.0;  // m' B (as k_bwd_gather formed it before)
-    }
-    __syncthreads();
-    // separable box (fixed order, deterministic): k-tap row sums of the L x TS columns the
-    // tile's outputs need, then k-tap column sums -- 2k adds per output instead of k^2
-    double* hA = tM + L * L;
-    double* hB = hA + L * TS;
-    double* hM = hB + L * TS;
-    for (int e = threadIdx.x; e < L * TS; e += 256) {
-        const int ry = e / TS, cx = e % TS;
-        double a = 0, b = 0, m = 0;
-        for (int jx = 0; jx < g.k; ++jx) {
-            const int f = ry * L + cx + jx;
-            a += tA[f];
-            b += tB[f];
-            m += tM[f];
-        }
-        hA[e] = a;
-        hB[e] = b;
-        hM[e] = m;
-    }
-    __syncthreads();
-    const int ly = threadIdx.x / TS, lx = threadIdx.x % TS;
-    const int64_t y = y0 + ly, x = x0 + lx;
-    if (y >= g.H || x >= g.W) return;
-    double sa = 0, sb = 0, sm = 0;
-    for (int i = 0; i < g.k; ++i) {
-        const int e = (ly + i) * TS + lx;
-        sa += hA[e];
-        sb += hB[e];
-        sm += hM[e];
-    }
-    const int64_t q = y * g.W + x;
-    const double ip = (double)to_f(img[q]) - (double)shift[side];
-    out[q] = (float)((double)T1[q] - sa - ip * sb + sm);
 }
 
 // grad(y,x) = T1 - Box[Z] - img'(y,x) Box[B]   (k_bwd_gather2's Z = A - m' B; one side per blockIdx.z)
@@ -1226,46 +1082,41 @@ struct BwdPlan {
     size_t part_bytes, acc_bytes, cover_bytes, prep_bytes, misc_bytes, rem_bytes;
 };
 
-// Host re-check of the slot bound: every column's cover count <= S (k_bwd_cover's own counting
-// code).  Cached per geometry -- the full layout's check is W x 2W/64 chunk tests.
-bool cover_fits(const Geo& g, int64_t dlo, int nChunk, int S, int Sj) {
-    struct Key {
-        int64_t W, D, dlo;
-        int r, layout, nChunk, S;
-        bool operator==(const Key& o) const {
-            return W == o.W && D == o.D && dlo == o.dlo && r == o.r && layout == o.layout && nChunk == o.nChunk &&
-                   S == o.S;
-        }
-    };
-    static std::mutex mu;
-    static std::vector<Key> good;
-    const Key key{g.W, g.D, dlo, g.r, g.layout, nChunk, S};
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        for (const Key& k : good)
-            if (k == key) return true;
-    }
-    for (int cls = 0; cls < 3; ++cls)
-        for (int64_t x = 0; x < g.W; ++x)
-            if (cover_column(g, dlo, nChunk, S, Sj, x, cls, nullptr) > S) return false;
-    std::lock_guard<std::mutex> lk(mu);
-    if (good.size() > 256) good.clear();
-    good.push_back(key);
-    return true;
-}
-
 // The window form's in-range offsets must stay below kWinNR: the gradient / volume rows one unit
 // reads (+ one row of columns and diagonals), and the six prepared images.
 bool win_path_ok(const Geo& g) {
-#ifdef CUSTMA_BWD_NOWIN
-    return false;
-#endif
     const double slab = (double)g.WO * (double)g.DO * 4.0;
     return g.layout == CUSTMA_LAYOUT_WINDOW && slab * (TRB + 2 * g.r + 2) < (double)kWinNR &&
            (double)g.H * (double)g.W * 24.0 < (double)kWinNR;
 }
 
+BwdPlan plan_bwd_uncached(const Geo& g);
+
+// plan_bwd runs from custma_workspace_bytes, backward_supported and the backward itself: the plans
+// of the last few geometries are kept (the full layout's chunk sweep is 2W/64 chunk ranges)
 BwdPlan plan_bwd(const Geo& g) {
+    struct Entry {
+        int64_t H, W, D, h_lo, h_hi;
+        int k, layout;
+        BwdPlan p;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (const Entry& e : cache)
+            if (e.H == g.H && e.W == g.W && e.D == g.D && e.h_lo == g.h_lo && e.h_hi == g.h_hi && e.k == g.k &&
+                e.layout == g.layout)
+                return e.p;
+    }
+    const BwdPlan p = plan_bwd_uncached(g);
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache.size() >= 16) cache.erase(cache.begin());
+    cache.push_back(Entry{g.H, g.W, g.D, g.h_lo, g.h_hi, g.k, g.layout, p});
+    return p;
+}
+
+BwdPlan plan_bwd_uncached(const Geo& g) {
     BwdPlan p;
     const int r = g.r;
     p.rem = false;
@@ -1275,8 +1126,7 @@ BwdPlan plan_bwd(const Geo& g) {
         p.jc = 0;
         // D = 64 n: the last diagonal alone would take a fifth chunk of sweeps with one live lane
         // in 64; k_bwd_rem_rows takes it instead (the window form only)
-        const char* er = getenv("CUSTMA_BWD_NOREM");  // benchmarking only
-        if (g.D >= NLB && (g.D + 1) % NLB == 1 && win_path_ok(g) && !(er && atoi(er) != 0)) {
+        if (g.D >= NLB && (g.D + 1) % NLB == 1 && win_path_ok(g)) {
             p.rem = true;
             p.nChunk -= 1;
         }
@@ -1316,9 +1166,11 @@ BwdPlan plan_bwd(const Geo& g) {
     } catch (...) {
         p.ok = false;
     }
+    // S = 2 x the max overlap bounds every column's cover count by construction (segment parity
+    // separates adjacent segments' ranges); k_bwd_cover still marks a column that would exceed it
+    // (count -1 -> NaN gradients in k_bwd_gather), the runtime guard that never drops a slot silently
     p.Sj = p.S;
     p.S = 2 * p.Sj;
-    if (p.ok && !cover_fits(g, p.dlo, p.nChunk, p.S, p.Sj)) p.ok = false;
     p.nsegMax = 1;
     for (int j = 0; j < p.nChunk; ++j) {
         const int ns = chunk_nseg(chunk_geo(g, p.dlo, j), r);
@@ -1363,7 +1215,7 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
                        cover);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // the patch sums (box, fp64, for k_bwd_combine2) and the six prepared fp32 images in one pass
+    // the patch sums (box, fp64, for k_bwd_gather) and the six prepared fp32 images in one pass
     // (stats.hip STATS_BWD_PREP; was box + sqt, then a separate k_bwd_prep pass over them)
     if ((e = launch_stats(cam, proj, std::is_same<T, __half>::value ? CUSTMA_F16 : CUSTMA_F32, g, sc, sp, s,
                           STATS_BWD_PREP, prep, shift)) != hipSuccess)
@@ -1375,7 +1227,6 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     a.S = p.S; a.Sj = p.Sj; a.nChunk = p.nChunk; a.nRG = p.nRG; a.jc = p.jc; a.nsegMax = p.nsegMax;
     a.dlo = p.dlo; a.ylo = p.ylo; a.yhi = p.yhi;
     a.order = g.layout == CUSTMA_LAYOUT_WINDOW ? 2 : 1;
-    if (const char* eo = getenv("CUSTMA_BWD_ORDER")) a.order = atoi(eo);  // benchmarking only
     a.remT = nullptr;
     a.remT1 = nullptr;
     if (p.rem) {
@@ -1421,14 +1272,8 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     }
     // (gather and combine fused into one tiled pass -- the slot sums recomputed for each tile's r
     // halo -- measured slower: C5 backward op 29.5 -> 31.1 ms, C2 full 3.82 -> 3.95 ms)
-    const int L = 16 + 2 * g.r;
-    const size_t lds = sizeof(double) * 3 * (L * L + L * 16);
-    const dim3 tiles((unsigned)cdiv(g.W, 16), (unsigned)cdiv(g.H, 16), 2);
     hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2), dim3(256), 0, s, g, a, acc,
                        a.remT, a.remT1);
-#ifdef CUSTMA_BWD_GATHER1
-    hipLaunchKernelGGL(k_bwd_combine2<T>, tiles, dim3(256), lds, s, g, cam, proj, shift, acc, sc, sp, dcam, dproj);
-#else
     {
         constexpr int TS3 = 32;
         const int L3 = TS3 + 2 * g.r;
@@ -1449,7 +1294,6 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
         }
         if (e != hipSuccess) return e;
     }
-#endif
     return hipGetLastError();
 }
 

@@ -84,9 +84,9 @@ void carve_stats(const Geo& g, void* ws, Stats* sc, Stats* sp) {
 }
 
 int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, void* ws, Stats* sc, Stats* sp,
-              hipStream_t s, int mode = STATS_FULL) {
+              hipStream_t s, int mode = STATS_FULL, int rows = STATS_ALL_ROWS) {
     carve_stats(g, ws, sc, sp);
-    return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s, mode), "stats");
+    return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s, mode, nullptr, nullptr, rows), "stats");
 }
 
 int check_dtype(int32_t dtype) {
@@ -225,7 +225,11 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     Stats sc, sp;
     const bool fast = precision == CUSTMA_FAST && fast_supported(g.k);
     // the fast sweeps read sq and box only; the exact forward reads mean and sq
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, fast ? STATS_FWD : STATS_FULL))) return rc;
+    // only the volume rows' statistics (a row band's halo rows feed the patches, not the statistics
+    // the sweeps read)
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, fast ? STATS_FWD : STATS_FULL,
+                        STATS_BAND_ROWS)))
+        return rc;
     if (fast)
         return check_hip(launch_fwd_fast(camera, projector, dtype, g, sc, sp, cost_volume, s), "forward(fast)");
     return check_hip(launch_fwd_exact(camera, projector, dtype, g, sc, sp, cost_volume, s), "forward(exact)");
@@ -328,7 +332,7 @@ int custma_disparity_band(const void* camera, const void* projector, int32_t dty
         return fail(CUSTMA_E_WORKSPACE, "workspace too small");
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, STATS_FULL, STATS_BAND_ROWS))) return rc;
     void* ws2 = (char*)workspace + stats_bytes(g);
     return check_hip(launch_disparity(camera, projector, dtype, g, sc, sp, index, best, n_rechecked, ws2, s, nullptr,
                                       0.f, nullptr, 0.f),
@@ -349,7 +353,7 @@ int custma_disparity_soft_band(const void* camera, const void* projector, int32_
         return fail(CUSTMA_E_WORKSPACE, "workspace too small");
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s))) return rc;
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, STATS_FULL, STATS_BAND_ROWS))) return rc;
     void* ws2 = (char*)workspace + stats_bytes(g);
     return check_hip(launch_disparity(camera, projector, dtype, g, sc, sp, index, best, n_rechecked, ws2, s, soft,
                                       beta, mask, threshold),

@@ -311,14 +311,12 @@ __device__ __forceinline__ double ld_bufs_f64(__amdgpu_buffer_rsrc_t r, uint32_t
 // Cache-policy bits of the volume stores (gfx950: 1 sc0, 2 nt, 16 sc1).  nt (streaming): the
 // volume is written once and far exceeds L2 / MALL, and keeping it out of L2 leaves the
 // sweep's image-statistics rows there (C3 window tile kernel 1.26 -> 1.10 ms on MI355X).
-#ifndef CUSTMA_STORE_AUX
-#define CUSTMA_STORE_AUX 2
-#endif
+constexpr int kStoreAux = 2;  // nt (sc1 alone and plain measured 2 % slower)
 __device__ __forceinline__ void st_buf(float v, __amdgpu_buffer_rsrc_t r, uint32_t off) {  // plain policy
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, 0);
 }
 __device__ __forceinline__ void st_vol(float v, __amdgpu_buffer_rsrc_t r, uint32_t off) {  // volume stores
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, CUSTMA_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, kStoreAux);
 }
 
 }  // namespace custma
@@ -337,10 +335,14 @@ hipError_t launch_u8_to_unit(const uint8_t* src, int64_t npix, int C, int ch, in
                              hipStream_t s);
 // Which statistics launch_stats writes (stats.hip k_stats): FULL = mean, sq, box, sqt; BOX = box, sqt (the
 // generic backward); BWD_PREP = box + the fused backward's prepared images (`prep`, needs `shift`); FWD = sq,
-// box (what the fast forward sweeps read).
+// box (what the fast forward sweeps read).  BAND: only the volume rows [h_lo, h_hi) (a forward or disparity
+// reads the statistics of its volume rows only: voxel (h, w, d) the camera's at (h, w), the projector's at
+// (h, d)); otherwise every image row (the backward reads its gradient rows and their halo).
 enum StatsMode { STATS_FULL = 0, STATS_BOX = 1, STATS_BWD_PREP = 2, STATS_FWD = 3 };
+enum StatsRows { STATS_ALL_ROWS = 0, STATS_BAND_ROWS = 1 };
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
-                        int mode = STATS_FULL, float* prep = nullptr, const float* shift = nullptr);
+                        int mode = STATS_FULL, float* prep = nullptr, const float* shift = nullptr,
+                        int rows = STATS_ALL_ROWS);
 hipError_t launch_fwd_exact(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             float* out, hipStream_t s);
 hipError_t launch_fwd_fast(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,

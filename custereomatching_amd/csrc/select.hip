@@ -310,7 +310,7 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
     // window layouts: the LDS-tiled merge while the projector strip fits
     const int ntx = (int)cdiv(g.WO, kMTX);
     const size_t mlds = sizeof(float) * (size_t)(kMTY + 2 * g.r) * (kMTX + 2 * g.r + (kMTX + g.D + 2 * g.r));
-    const bool mtile = g.layout == CUSTMA_LAYOUT_WINDOW && mlds <= 48 * 1024 && !getenv("CUSTMA_DISP_MERGE_FLAT");
+    const bool mtile = g.layout == CUSTMA_LAYOUT_WINDOW && mlds <= 48 * 1024;
     const unsigned mtb = (unsigned)(ntx * cdiv(g.HV(), kMTY));
     auto merge = [&](auto kc) {
         constexpr int KT = decltype(kc)::value;

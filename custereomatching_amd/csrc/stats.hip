@@ -41,7 +41,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <typename T, int KT, int MODE>
 __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const T* __restrict__ img1, Geo g,
                                                Stats st0, Stats st1, float* __restrict__ prep,
-                                               const float* __restrict__ shift) {
+                                               const float* __restrict__ shift, int64_t ybeg, int64_t yend) {
     constexpr bool BOX_ONLY = MODE == STATS_BOX || MODE == STATS_BWD_PREP;
     // blockIdx.z: 0 = camera, 1 = projector (one launch for both images)
     const T* __restrict__ img = blockIdx.z ? img1 : img0;
@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
     double* rs = lds_d;                    // [LY][TX] fp64 k-tap row sums
     double* rs2 = rs + LY * TX;            // [LY][TX] fp64 k-tap row sums of squares
     float* tile = (float*)(rs2 + LY * TX);  // [LY][LX] zero-padded image tile
-    const int64_t y0 = (int64_t)blockIdx.y * TY, x0 = (int64_t)blockIdx.x * TX;
+    // pixel rows [ybeg, yend) (STATS_BAND_ROWS: the volume rows only)
+    const int64_t y0 = ybeg + (int64_t)blockIdx.y * TY, x0 = (int64_t)blockIdx.x * TX;
     for (int e = threadIdx.x; e < LY * LX; e += 256) {
         const int ty = e / LX, tx = e % LX;
         tile[e] = ldpad(img, g.H, g.W, y0 + ty - r, x0 + tx - r);
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
         for (int p = 0; p < PR; ++p) {
             const int ly = PR * q + p;
             const int64_t y = y0 + ly;
-            if (y >= g.H) break;
+            if (y >= yend) break;
             double b = 0.0, b2 = 0.0;
 #pragma unroll
             for (int i = 0; i < k; ++i) {
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
     for (int p = 0; p < PR; ++p) {
         const int ly = PR * q + p;
         const int64_t y = y0 + ly;
-        if (y >= g.H) break;
+        if (y >= yend) break;
         double b = 0.0, b2 = 0.0;
 #pragma unroll
         for (int i = 0; i < k; ++i) {
@@ -213,8 +214,10 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
 }  // namespace
 
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
-                        int mode, float* prep, const float* shift) {
-    const dim3 grid((unsigned)cdiv(g.W, TX), (unsigned)cdiv(g.H, TY), 2);
+                        int mode, float* prep, const float* shift, int rows) {
+    const int64_t ybeg = rows == STATS_BAND_ROWS ? g.h_lo : 0, yend = rows == STATS_BAND_ROWS ? g.h_hi : g.H;
+    if (yend <= ybeg || g.W == 0) return hipSuccess;
+    const dim3 grid((unsigned)cdiv(g.W, TX), (unsigned)cdiv(yend - ybeg, TY), 2);
     const int LX = TX + 2 * g.r, LY = TY + 2 * g.r;
     const size_t lds = sizeof(double) * 2 * LY * TX + sizeof(float) * LY * LX;
     hipError_t err = hipSuccess;
@@ -225,7 +228,7 @@ hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo&
             constexpr int M = decltype(mc)::value;
             if ((err = allow_lds(k_stats<T, KT, M>, lds)) != hipSuccess) return;
             hipLaunchKernelGGL((k_stats<T, KT, M>), grid, dim3(256), lds, s, (const T*)cam, (const T*)proj, g, sc, sp,
-                               prep, shift);
+                               prep, shift, ybeg, yend);
         };
         auto by_mode = [&](auto* cast) {
             switch (mode) {

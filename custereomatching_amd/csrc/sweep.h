@@ -165,11 +165,7 @@ inline SweepGrid sweep_grid(const Geo& g, bool owned = false) {
     // cost = diagonal lanes launched, penalised for single-wave workgroups
     double best = 1e300;
     sg.NL = 256;
-    // tuning override (benchmarking only): CUSTMA_SWEEP_NW
-    const char* enw = getenv("CUSTMA_SWEEP_NW");
-    const int nw_fix = enw ? atoi(enw) : 0;
     for (int nw = 1; nw <= 5; ++nw) {
-        if (nw_fix && nw != nw_fix) continue;
         if (owned && 64 * nw <= margin) continue;
         if (!owned && g.layout != CUSTMA_LAYOUT_WINDOW && nw > 4) continue;
         const int64_t per = owned ? 64 * nw - margin : 64 * nw;

@@ -42,12 +42,10 @@ namespace custma {
 namespace {
 
 typedef __attribute__((address_space(3))) volatile double lds_vd;
-#ifndef CUSTMA_FWD_NST
-#define CUSTMA_FWD_NST 2  // loader register stages (x loads per step <= 63 + one step)
-#endif
+constexpr int kFwdNST = 2;  // loader register stages (x loads per step <= 63 + one step)
 
 
-template <int K, int TWT, typename T, bool ARGMAX, bool DIRECT>
+template <int K, int TWT, typename T, bool ARGMAX>
 __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                    Stats sc, Stats sp, float* __restrict__ out, SweepGrid sg,
                                                    DispPartial part) {
@@ -116,7 +114,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         // Raw bits only: nothing consumes a load in the step that issues it, and every load is
         // unconditional (unused lanes / chunks carry the out-of-range offset), so the loads of
         // three steps stay in flight (the compiler's vmcnt waits only for the oldest stage).
-        constexpr int NST = CUSTMA_FWD_NST;
+        constexpr int NST = kFwdNST;
         struct Stage {
             uint32_t ue, ul, oe[LO], ol[LO], q[LS], uq;
             double m[LS], ub;
@@ -291,12 +289,6 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             voff[m] = ok ? (uint32_t)((m * DO + cb + tid) * 4) : OOB;
         }
     }
-    uint32_t dvoff[TWT];  // DIRECT: this lane's column (window offset d0 + tid) in tile row m
-#pragma unroll
-    for (int m = 0; m < TWT; ++m) {
-        const bool ok = DIRECT && u0 + m < g.WO && d0 + tid < (int64_t)DO;
-        dvoff[m] = ok ? (uint32_t)((m * DO + d0 + tid) * 4) : OOB;
-    }
     // staging index of column c in row m: m*NL + c - d0 - (u0 + m) (full) / m*NL + c - d0
     // (window); with c = voff/4 - m*DO that is voff/4 + m*stgA + stgB
     const int stgA = NL - DO - (window ? 0 : 1), stgB = -(int)d0 - (window ? 0 : (int)u0);
@@ -306,30 +298,18 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         float v[TWT];
 #pragma unroll
         for (int m = 0; m < TWT; ++m) v[m] = *(const float*)(tile + voff[m] + 4 * (m * stgA + stgB));
-#ifndef CUSTMA_ABL_NOSTORE  // ablation builds only (scripts/build_ablations.py)
 #pragma unroll
         for (int m = 0; m < TWT; ++m) st_vol(v[m], rOut, voff[m]);
-#else
-#pragma unroll
-        for (int m = 0; m < TWT; ++m)
-            if (v[m] == 1234.5f) st_vol(v[m], rOut, voff[m]);
-#endif
     };
 
     __syncthreads();  // the loader's first stage
     for (int64_t h = hs; h < h1; ++h) {
         const int buf = (int)((h - hs) & 1);
-        if constexpr (!ARGMAX && !DIRECT) {
+        if constexpr (!ARGMAX) {
             if (h > h0) store_tile(h - 1, buf ^ 1);
         }
-#ifndef CUSTMA_ABL_NOUPDATE  // ablation builds only (scripts/build_ablations.py)
         update(buf);
-#endif
-#ifdef CUSTMA_ABL_NOOUT
-        if (h >= h0 && ARGMAX) {
-#else
         if (h >= h0) {
-#endif
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
 #pragma unroll
             for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
@@ -347,10 +327,6 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             while (TPR * 2 * TWT <= NL && TPR < 16) TPR *= 2;
             const int NLP = ARGMAX ? NL + TPR : NL;
             float* srow = stg + (ARGMAX ? 0 : buf * 16 * NL) + tid;
-            // DIRECT (window layout, one chunk of diagonals): lane tid holds volume column
-            // d0 + tid of the 16 rows u0 .. u0+15, so each m is one 256-byte store from the
-            // registers -- no LDS staging, which leaves room for more workgroups per CU
-            const auto rOutD = make_rsrc(out + ((h - g.h_lo) * g.WO + u0) * g.DO, 0x7FFFFFF0u);
             Unroll<0, TWT>::run([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
                 if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
@@ -361,8 +337,6 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
                 if constexpr (ARGMAX) {
                     srow[m * NLP] = (m >= m_lo && m < m_hi) ? c : -FLT_MAX;
-                } else if constexpr (DIRECT) {
-                    if (h >= h0) st_vol(c, rOutD, dvoff[m]);
                 } else {
                     srow[m * NL] = c;
                 }
@@ -432,52 +406,31 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         __syncthreads();
     }
     if constexpr (!ARGMAX) {
-        if constexpr (!DIRECT) {
-            if (h1 > h0) store_tile(h1 - 1, (int)((h1 - 1 - hs) & 1));
-        }
+        if (h1 > h0) store_tile(h1 - 1, (int)((h1 - 1 - hs) & 1));
         __syncthreads();
     }
-}
-
-// DIRECT stores (see the kernel): window layout whose D+1 diagonals fit one chunk of at most
-// 320 lanes.  Off by default: on 2048^2 D=256 k=11 it measured 2.56 ms against 2.34 ms for the
-// LDS-staged sector-owned stores.  CUSTMA_FWD_DIRECT=1 enables it (benchmarking only).
-inline bool use_direct(const Geo& g) {
-    const char* e = getenv("CUSTMA_FWD_DIRECT");
-    return e && atoi(e) != 0 && g.layout == CUSTMA_LAYOUT_WINDOW && g.DO <= 320;
 }
 
 template <int K, typename T>
 hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out,
                     DispPartial* part, hipStream_t s) {
-    const bool direct = part == nullptr && use_direct(g);
-    SweepGrid sg = sweep_grid(g, /*owned=*/part == nullptr && !direct);
-    if (direct) {  // one chunk covering all D+1 diagonals
-        sg.NL = (int)cdiv(g.DO, 64) * 64;
-        sg.S = sg.NL;
-        sg.nChunk = 1;
-        sg.TH = 64;
-        while (sg.TH > 8 && (int64_t)sg.nTile * cdiv(g.HV(), sg.TH) < 4096) sg.TH /= 2;
-        sg.nBand = (int)cdiv(g.HV(), sg.TH);
-    }
+    // (per-lane 256-byte stores straight from registers, one chunk of all D+1 diagonals of a window,
+    // measured slower: 2.56 vs 2.34 ms at 2048^2, D = 256, k = 11)
+    const SweepGrid sg = sweep_grid(g, /*owned=*/part == nullptr);
     constexpr int R = K / 2, NX = TW + 2 * R;
     constexpr int NL_MAX = 320, OP = 64 * ((NX + NL_MAX - 1 + 63) / 64), SP = 64 * ((TW + NL_MAX - 1 + 63) / 64);
     const int NL = sg.NL;
     const size_t lds = sizeof(double) * (4 * OP + 2 * 64 + 2 * SP + 2 * 64) +
-                       sizeof(float) * (2 * SP + 2 * 64 + (direct ? 0 : part ? TW * (NL + 16) : 2 * TW * NL));
+                       sizeof(float) * (2 * SP + 2 * 64 + (part ? TW * (NL + 16) : 2 * TW * NL));
     const int64_t blocks = sweep_blocks(sg);
     if (part) {
-        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam,
+        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam,
                            proj, g, sc, sp, out, sg, *part);
     } else {
         DispPartial none{};
         prof_begin(PROF_FWD, s);
-        if (direct)
-            hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false, true>), dim3((unsigned)blocks), dim3(NL + 64), lds, s,
-                               cam, proj, g, sc, sp, out, sg, none);
-        else
-            hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s,
-                               cam, proj, g, sc, sp, out, sg, none);
+        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam, proj,
+                           g, sc, sp, out, sg, none);
         prof_end(PROF_FWD, s);
     }
     return hipGetLastError();

@@ -47,14 +47,8 @@ typedef __attribute__((address_space(3))) volatile float lds_vf;
 constexpr int kRowP = 128;  // LDS row stride (>= 16 + 2r + 63)
 // The row update's DPP FMAs keep their `s_nop 1` only where a camera operand may have just
 // been converted (the first group of each 16-column half); hazard_check.py checks the
-// listing at build time.  CUSTMA_DPP_NOP=1 puts them back everywhere (benchmarking)
-#ifndef CUSTMA_DPP_NOP
-#define CUSTMA_DPP_NOP 0
-#endif
-constexpr bool kDppNop = CUSTMA_DPP_NOP != 0;
-#ifndef CUSTMA_FWD_PF
-#define CUSTMA_FWD_PF 2  // outputs whose statistics are read ahead
-#endif
+// listing at build time.
+constexpr int kFwdPF = 2;  // outputs whose projector statistics are read ahead from LDS
 
 // REM: this wave (window layout, last chunk, (D+1) % 64 == 1) also computes the single
 // remainder diagonal d0 + 64 = D: lane x < 16 + 2r keeps its column sum, the horizontal box
@@ -104,20 +98,11 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         return (have && x >= 0 && x < g.W) ? (uint32_t)(x * esz) : OOB;
     };
     const int64_t xO0 = u0 - R + d0, oS = u0 + d0;
-    uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 64, xO0 + 64 + l, sizeof(T));
-    uint32_t vC0 = colOff(true, u0 - R + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R + 16 + r16, sizeof(T));
-    uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 64, oS + 64 + l, 8);
-    uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 64, oS + 64 + l, 4);
-    uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
-#ifdef CUSTMA_ABL_NOSTATSMEM  // ablation (timing only): statistics loads out of range (no memory access)
-    vM0 = vM1 = vQ0 = vQ1 = vUB = vUQ = OOB;
-#endif
-#ifdef CUSTMA_ABL_NOCAMMEM  // ablation (timing only): camera image-row and statistics loads out of range
-    vC0 = vC1 = vUB = vUQ = OOB;
-#endif
-#ifdef CUSTMA_ABL_NOIMGMEM  // ablation (timing only): image-row loads out of range
-    vP0 = vP1 = vC0 = vC1 = OOB;
-#endif
+    const uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 64, xO0 + 64 + l, sizeof(T));
+    const uint32_t vC0 = colOff(true, u0 - R + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R + 16 + r16, sizeof(T));
+    const uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 64, oS + 64 + l, 8);
+    const uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 64, oS + 64 + l, 4);
+    const uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
     // Rows by SGPR soffset from one descriptor per array, based at the band's first row rb
     // (so every offset stays small whatever the image size); a row outside the image gets
     // soffset OOBS, past num_records (<= OOBS), so its loads read 0 -- also when the lane's
@@ -194,7 +179,6 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     double col[NX];
 #pragma unroll
     for (int x = 0; x < NX; ++x) col[x] = 0.0;
-    float sink = 0.f;   // CUSTMA_ABL_NOSTORE: keeps the outputs live
     double colR = 0.0;  // REM: column sum of diagonal d0 + 64 for column x = lane (lanes < NX)
 
     // The loads of step t are issued at the end of step t-P (P = 2, or 3 in the staged
@@ -204,37 +188,19 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     // issues, so a peeled prologue with another register assignment would be joined to the
     // loop by register copies -- reads of registers whose loads are still in flight.
     Stage st[P];
-    // EARLY: a step's loads (for step t + P) issued right after its barrier, before its block
-    // stores, so the wait for loads(t) does not wait for the stores of step t - 2.  Measured
-    // no faster on MI355X (C3 volume 1.257 vs 1.226 ms, the fused disparity 22 % slower), so
-    // off unless built with CUSTMA_TILE_EARLY (benchmarking only).
-#if defined(CUSTMA_TILE_EARLY) && !defined(CUSTMA_ABL_NOSTORE)
-    constexpr bool EARLY = STAGED && P == 2 && AMX == 0;
-#else
-    constexpr bool EARLY = false;
-#endif
     auto compute = [&](Stage& p, int64_t t) {
         // loads(t) were issued at the end of step t-P; after them, for each step s in
         // t-P+1 .. t-1: its stores (from step h0 on) and loads(s+P)
         constexpr int ST = AMX > 0 ? (SOFT ? 5 : 3) * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);
-        static_assert((P - 1) * (kLoads + ST) + (EARLY ? ST : 0) <= 63, "vmcnt holds the pipeline");
-#ifdef CUSTMA_ABL_NOWAIT  // ablation builds only: no wait for the loads (garbage values)
-        asm_vmcnt<63>();
-#else
+        static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
         if constexpr (P == 3) {
             if (t - 2 >= h0) asm_vmcnt<2 * (kLoads + ST)>();
             else if (t - 1 >= h0) asm_vmcnt<2 * kLoads + ST>();
             else asm_vmcnt<2 * kLoads>();
-        } else if constexpr (EARLY) {
-            // issued after loads(t): stores(t-2), loads(t+1), stores(t-1)
-            if (t - 2 >= h0) asm_vmcnt<kLoads + 2 * ST>();
-            else if (t - 1 >= h0) asm_vmcnt<kLoads + ST>();
-            else asm_vmcnt<kLoads>();
         } else {
             if (t - 1 >= h0) asm_vmcnt<kLoads + ST>();
             else asm_vmcnt<kLoads>();
         }
-#endif
         tie(p);
         rowE[l] = raw_to_f64<T>(p.pe0);
         rowE[64 + l] = raw_to_f64<T>(p.pe1);
@@ -262,7 +228,6 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         const float uq = __builtin_bit_cast(float, p.uq);  // camera ex2 of column r16
 
         // ---- col[x] += c(enter, x) p(enter, x + delta) - c(leave, x) p(leave, x + delta) ----
-#ifndef CUSTMA_ABL_NOUPDATE  // ablation builds only (scripts/build_ablations.py)
         {
             const lds_vd* oa = (const lds_vd*)(rowE + l);
             const lds_vd* ob = (const lds_vd*)(rowL + l);
@@ -286,20 +251,19 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 const double* qa = pa[bb & 1];
                 const double* qb = pb[bb & 1];
                 if constexpr (nb_ == 4) {
-                    fmac2_bc64_x4<(x0 & 15), kDppNop || x0 == 0 || x0 == 16>(col[x0], col[x0 + 1], col[x0 + 2], col[x0 + 3], a, b, qa[0], qa[1],
+                    fmac2_bc64_x4<(x0 & 15), x0 == 0 || x0 == 16>(col[x0], col[x0 + 1], col[x0 + 2], col[x0 + 3], a, b, qa[0], qa[1],
                                              qa[2], qa[3], qb[0], qb[1], qb[2], qb[3]);
                 } else if constexpr (nb_ == 2) {
-                    fmac2_bc64_x2<(x0 & 15), kDppNop || x0 == 0 || x0 == 16>(col[x0], col[x0 + 1], a, b, qa[0], qa[1], qb[0], qb[1]);
+                    fmac2_bc64_x2<(x0 & 15), x0 == 0 || x0 == 16>(col[x0], col[x0 + 1], a, b, qa[0], qa[1], qb[0], qb[1]);
                 } else {
                     Unroll<0, nb_>::run([&](auto ic) {
                         constexpr int i = decltype(ic)::value, x = x0 + i;
-                        fmac_bc64<(x & 15), kDppNop || x0 == 0 || x0 == 16>(col[x], a, qa[i]);
-                        fmac_bc64<(x & 15), kDppNop || x0 == 0 || x0 == 16>(col[x], b, qb[i]);
+                        fmac_bc64<(x & 15), x0 == 0 || x0 == 16>(col[x], a, qa[i]);
+                        fmac_bc64<(x & 15), x0 == 0 || x0 == 16>(col[x], b, qb[i]);
                     });
                 }
             });
         }
-#endif
 
         if constexpr (REM) {
             const double cRe = l < 16 ? ca0 : ca1, cRl = l < 16 ? cb0 : cb1;  // camera column u0 - R + l
@@ -318,7 +282,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             typedef __attribute__((address_space(3))) const float lds_f;
             const lds_d* mrow = (const lds_d*)(sM + l);
             const lds_f* qrow = (const lds_f*)(sQ + l);
-            constexpr int PF = CUSTMA_FWD_PF;
+            constexpr int PF = kFwdPF;
             double mq[PF];
             float qq[PF];
             Unroll<0, PF>::run([&](auto ic) {
@@ -346,27 +310,17 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 }
                 // E + eps = S + eps - box_c * mean_p;  ex2 * ey2 + eps
                 fin_bc<m>(e, den2, s, nb, mv, uq, qv);
-#ifdef CUSTMA_ABL_NOOUT
-                const float c = (float)m;
-#else
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
-#endif
                 uint32_t vo = vOut, so = (uint32_t)(m * sstep);
                 if constexpr (FULL_EDGE) {  // per-row mask; the whole offset in voffset
                     vo = ((uint64_t)(a0 + m) < (uint64_t)g.W) ? (uint32_t)((a0 + m + m * DO) * 4) : OOB;
                     so = 0;
                 }
-#ifdef CUSTMA_ABL_NOSTORE
-                sink += c;
-                (void)dv;
-                (void)sb;
-#else
                 if constexpr (STAGED) {
                     if (!MASKED || dv) sb[m * DO + d0 + l] = c;
                 } else
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, so,
-                                                      CUSTMA_STORE_AUX);
-#endif
+                                                      kStoreAux);
             });
             };
             if (!STAGED || allv) outputs(std::false_type{});
@@ -386,15 +340,13 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 } else {
                     const uint32_t vo = l < 16 ? (uint32_t)((l * DO + g.D) * 4) : OOB;
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, 0u,
-                                                          CUSTMA_STORE_AUX);
+                                                          kStoreAux);
                 }
             }
-#ifndef CUSTMA_ABL_NOSTORE
             if constexpr (STAGED) {
                 // every wave's part of the 16 rows is in LDS: store the block (256 contiguous
                 // bytes per wave instruction, the whole workgroup's instruction contiguous)
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                if constexpr (EARLY) load_step(t + P, p);  // p is dead past the outputs
                 const int NT = (int)blockDim.x, tid = (int)threadIdx.x;
                 const int total = (int)(nrow * DO);
                 if constexpr (AMX > 0) {
@@ -461,13 +413,13 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                         const int j = i * NT + tid;
                         const i32x4 v = ((lds_v4*)sb)[j < n4 ? j : 0];
                         __builtin_amdgcn_raw_buffer_store_b128(v, rOut, j < n4 ? (uint32_t)(j * 16) : OOB, 0u,
-                                                               CUSTMA_STORE_AUX);
+                                                               kStoreAux);
                     }
                     const int j = 4 * n4 + tid;
                     const float v = sb[j < total ? j : 0];
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), rOut,
                                                           (tid < 4 && j < total) ? (uint32_t)(j * 4) : OOB, 0u,
-                                                          CUSTMA_STORE_AUX);
+                                                          kStoreAux);
                 } else {
 #pragma unroll
                     for (int i = 0; i < SS; ++i) {
@@ -475,18 +427,17 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                         const float v = sb[idx < total ? idx : 0];
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), rOut,
                                                               idx < total ? (uint32_t)(idx * 4) : OOB, 0u,
-                                                              CUSTMA_STORE_AUX);
+                                                              kStoreAux);
                     }
                 }
             }
-#endif
         }
     };
     auto step = [&](auto kc, int64_t t) {
         Stage& p = st[decltype(kc)::value];
         if (t >= hs) compute(p, t);
         // past the band's end: harmless (rows out of range read zeros)
-        if (!(EARLY && t >= h0)) load_step(t + P, p);
+        load_step(t + P, p);
     };
     int64_t t_first = hs - P;  // opaque: the warm-up iterations must not be peeled
     asm volatile("" : "+s"(t_first));
@@ -501,9 +452,6 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         }
     }
     asm_vmcnt<0>();  // every wave drains its own loads before it ends
-#ifdef CUSTMA_ABL_NOSTORE
-    if (sink == 1.2345f) out[l] = sink;
-#endif
 }
 
 template <int K, typename T>
@@ -535,10 +483,7 @@ __global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, cons
 // Window layout, D + 1 <= 64 * kTileMaxChunks (+1): one workgroup per (column tile, row
 // band) holding all diagonal chunks, wave w = chunk w (the last one also takes the
 // remainder diagonal when wg.rem); outputs leave through the LDS block image (STAGED).
-#ifndef CUSTMA_TILE_P
-#define CUSTMA_TILE_P 2
-#endif
-constexpr int kTileP = CUSTMA_TILE_P;  // load pipeline depth (steps)
+constexpr int kTileP = 2;  // load pipeline depth (steps; 3 measured no faster)
 constexpr int kWaveLds = (3 * kRowP + 64) * 8 + kRowP * 4;  // rowE, rowL, sM, sR (f64) + sQ (f32)
 
 template <int K, typename T, bool X4, int AMX = 0, bool CPL = false>
@@ -578,8 +523,8 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
 }
 
 // CPL: fp16 images, when the camera block keeps the tile kernel at three workgroups per CU (LDS
-// <= 160 KiB / 3); CUSTMA_FWD_CPL=0 turns it off (benchmarking only).  Volume form: C5 9.81 -> 9.15 ms,
-// C3 unchanged (profiles/r03/cpl); the fused disparity keeps its per-step camera loads.
+// <= 160 KiB / 3).  Volume form: C5 9.81 -> 9.15 ms, C3 unchanged (profiles/r03/cpl); the fused
+// disparity keeps its per-step camera loads (3 % slower with the preload).
 template <int K, typename T>
 size_t cpl_bytes(const WaveGrid& wg) {
     constexpr int R = K / 2, NX = TW + 2 * R;
@@ -588,16 +533,13 @@ size_t cpl_bytes(const WaveGrid& wg) {
 template <int K, typename T>
 bool cpl_ok(const Geo& g, const WaveGrid& wg, size_t lds) {
     (void)g;
-    const char* e = getenv("CUSTMA_FWD_CPL");
-    if (e && atoi(e) == 0) return false;
     return sizeof(T) == 2 && lds + cpl_bytes<K, T>(wg) <= 163840 / 3;
 }
 
 template <int K, typename T>
 hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out, hipStream_t s) {
     const WaveGrid wg = wave_grid(g);
-    const char* e = getenv("CUSTMA_FWD_TILE");  // benchmarking only: 0 = per-wave kernel
-    const bool tile = g.layout == CUSTMA_LAYOUT_WINDOW && wg.nChunk <= kTileMaxChunks && !(e && atoi(e) == 0);
+    const bool tile = g.layout == CUSTMA_LAYOUT_WINDOW && wg.nChunk <= kTileMaxChunks;
     prof_begin(PROF_FWD, s);
     if (tile) {
         const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
@@ -606,8 +548,7 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
         if (cpl) lds += cpl_bytes<K, T>(wg);
         // 16-byte stores when every block base is 16-byte aligned: out aligned and
         // ((t - h_lo) WO + u0) DO = 0 mod 4 for all t (u0 = 0 mod 16)
-        const char* e4 = getenv("CUSTMA_FWD_X4");  // benchmarking only: 0 = dword stores
-        const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0) && !(e4 && atoi(e4) == 0);
+        const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0);
         const dim3 blk(64 * wg.nChunk);
         if (x4 && cpl) {
             if constexpr (sizeof(T) == 2)
@@ -633,22 +574,13 @@ template <int K, typename T>
 hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, DispPartial part, hipStream_t s) {
     const WaveGrid wg = wave_grid(g);
     const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
-    size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
-    // the camera preload measured slower here (C5 9.69 -> 9.99 ms, C3 1.15 -> 1.18 ms): opt-in only
-    const char* ec = getenv("CUSTMA_DISP_CPL");
-    const bool cpl = ec && atoi(ec) != 0 && cpl_ok<K, T>(g, wg, lds);
-    if (cpl) lds += cpl_bytes<K, T>(wg);
+    // (no camera preload here: it measured slower, C5 9.69 -> 9.99 ms, C3 1.15 -> 1.18 ms)
+    const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
     prof_begin(PROF_FWD, s);
     const int passes = wg.nChunk == 4 ? 1 : wg.nChunk >= 2 ? 2 : 4;  // 16 rows over the waves, 4 per pass
     auto go = [&](auto amx) {
-        if (cpl) {
-            if constexpr (sizeof(T) == 2)
-                hipLaunchKernelGGL((k_fwd_tile<K, T, false, decltype(amx)::value, true>), dim3((unsigned)blocks),
-                                   dim3(64 * wg.nChunk), lds, s, cam, proj, g, sc, sp, nullptr, wg, part);
-        } else {
-            hipLaunchKernelGGL((k_fwd_tile<K, T, false, decltype(amx)::value>), dim3((unsigned)blocks),
-                               dim3(64 * wg.nChunk), lds, s, cam, proj, g, sc, sp, nullptr, wg, part);
-        }
+        hipLaunchKernelGGL((k_fwd_tile<K, T, false, decltype(amx)::value>), dim3((unsigned)blocks),
+                           dim3(64 * wg.nChunk), lds, s, cam, proj, g, sc, sp, nullptr, wg, part);
     };
     const bool soft = part.s0 != nullptr;  // soft-argmax sums requested
     if (passes == 1) soft ? go(std::integral_constant<int, -1>{}) : go(std::integral_constant<int, 1>{});
@@ -687,12 +619,10 @@ WaveGrid wave_grid(const Geo& g) {
     wg.nChunk = (int)cdiv(nd, 64);
     // window with (D+1) % 64 == 1 (D = 64 n): the last full chunk's waves also compute the
     // single remainder diagonal D (no fifth, nearly idle chunk of waves)
-    wg.rem = g.layout == CUSTMA_LAYOUT_WINDOW && nd > 64 && nd % 64 == 1 && !getenv("CUSTMA_WAVE_NOREM");
+    wg.rem = g.layout == CUSTMA_LAYOUT_WINDOW && nd > 64 && nd % 64 == 1;
     if (wg.rem) --wg.nChunk;
     wg.nTile = (int)cdiv(g.WO, TW);
-    // tuning override (benchmarking only): CUSTMA_WAVE_TH
-    const char* e = getenv("CUSTMA_WAVE_TH");
-    wg.TH = e && atoi(e) > 0 ? atoi(e) : 64;
+    wg.TH = 64;  // band height (32 / 128 measured within 2 %)
     // keep >= ~8 waves per SIMD on small problems
     while (wg.TH > 8 && (int64_t)wg.nTile * wg.nChunk * cdiv(g.HV(), wg.TH) < 8192) wg.TH /= 2;
     wg.nBand = (int)cdiv(g.HV(), wg.TH);
@@ -700,8 +630,7 @@ WaveGrid wave_grid(const Geo& g) {
 }
 
 bool disp_tile_ok(const Geo& g) {
-    const char* e = getenv("CUSTMA_FWD_TILE");  // benchmarking only: 0 = the LDS-form partials
-    return g.layout == CUSTMA_LAYOUT_WINDOW && wave_grid(g).nChunk <= kTileMaxChunks && !(e && atoi(e) == 0);
+    return g.layout == CUSTMA_LAYOUT_WINDOW && wave_grid(g).nChunk <= kTileMaxChunks;
 }
 
 hipError_t launch_disp_tile(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,

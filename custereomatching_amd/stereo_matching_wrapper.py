@@ -187,10 +187,12 @@ class _StereoMatching(torch.autograd.Function):
     Saves only the two images, as the reference does (:16).  The backward also
     needs the forward's costs (V = g * cost / S); it reads the returned volume
     when that tensor is still alive and unmodified (a weak reference plus its
-    version counter -- no reference cycle, no extra lifetime), and otherwise
-    recomputes the volume inside the backward call (CUSTMA_OP_BACKWARD_RECOMPUTE).
-    So an in-place edit of the returned volume, or dropping it before
-    ``.backward()``, behaves as with the reference."""
+    version counter -- no reference cycle, no extra lifetime).  Otherwise it
+    recomputes the volume here, with ``cost_volume_forward`` and the precision
+    the forward used, into a transient tensor of the volume's size (4 bytes per
+    voxel, e.g. 33 GB at 4096 x 8192 with D = 256), and passes it to the
+    library.  So an in-place edit of the returned volume, or dropping it before
+    ``.backward()``, behaves as with the reference, at that peak-memory cost."""
 
     @staticmethod
     def forward(ctx, camera_image, projector_image, D, kernel_size, layout="full", precision=None):

@@ -1,0 +1,133 @@
+// Store-shape microbenchmark for the window-layout volume (diagnostic only, round 4).
+// C3 window geometry (H 2048, WO 1792, DO 257, fp32 = 3.77 GB).  Each workgroup owns a
+// (TW-column tile, TH-row band) and, per step (volume row), writes the tile's contiguous
+// TW * DO-float block; nothing is computed.  Variants: store width (dword / dwordx4), cache
+// policy, a barrier per step or not, blocks of 1 or 2 steps per burst, workgroups per CU
+// (dynamic LDS padding), tile width 16 / 32, and grid-stride baselines.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
+    const int64_t q = nb / 8, rem = nb % 8, x = b % 8, i = b / 8;
+    return x < rem ? x * (q + 1) + i : rem * (q + 1) + (x - rem) * q + i;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)n, 0x00020000);
+}
+
+// X4: 16-byte stores; AUX: cache-policy bits (2 = nt); BAR: barrier per burst; STEPS: volume rows
+// per burst (the block of STEPS rows is written after STEPS steps)
+template <bool X4, int AUX, bool BAR, int STEPS, int TW>
+__global__ __launch_bounds__(256) void k_tile(float* out, int64_t H, int64_t WO, int64_t DO, int TH, int nTile) {
+    extern __shared__ float pad[];
+    if (threadIdx.x == 1000) pad[0] = 0.f;  // dynamic LDS only sets the occupancy
+    const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int wt = (int)(bid % nTile), band = (int)(bid / nTile);
+    const int64_t u0 = (int64_t)wt * TW;
+    const int nrow = (int)min((int64_t)TW, WO - u0);
+    const int total = nrow * (int)DO;
+    const int tid = threadIdx.x;
+    const int64_t t0 = (int64_t)band * TH, t1 = min(H, t0 + TH);
+    for (int64_t t = t0; t < t1; t += STEPS) {
+#pragma unroll
+        for (int s = 0; s < STEPS; ++s) {
+            if (t + s >= t1) break;
+            float* blk = out + ((t + s) * WO + u0) * DO;
+            const auto r = rsrc(blk, (uint32_t)(total * 4));
+            if constexpr (X4) {
+                const int n4 = total >> 2;
+                for (int j = tid; j < n4 + 1; j += 256) {
+                    if (j < n4) {
+                        const i32x4 v = {j, j, j, (int)t};
+                        __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)(j * 16), 0u, AUX);
+                    } else if (tid < 256) {
+                        for (int q = 4 * n4; q < total; ++q) blk[q] = 1.f;
+                    }
+                }
+            } else {
+                for (int j = tid; j < total; j += 256)
+                    __builtin_amdgcn_raw_buffer_store_b32((unsigned)j, r, (uint32_t)(j * 4), 0u, AUX);
+            }
+        }
+        if (BAR) __syncthreads();
+    }
+}
+template <int AUX>
+__global__ void k_dword(float* out, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t st = (int64_t)gridDim.x * blockDim.x;
+    const auto r = rsrc(out, 0x7FFFFFF0u);
+    for (; i < n; i += st) {
+        if (i * 4 < 0x7FFFFFF0) __builtin_amdgcn_raw_buffer_store_b32(1u, r, (uint32_t)(i * 4), 0u, AUX);
+        else out[i] = 1.f;
+    }
+}
+template <int AUX>
+__global__ void k_x4(float* out, int64_t n4) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t st = (int64_t)gridDim.x * blockDim.x;
+    for (; i < n4; i += st) {
+        const i32x4 v = {1, 2, 3, 4};
+        const auto r = rsrc(out + i * 4, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, 0u, 0u, AUX);
+    }
+}
+
+int main() {
+    const int64_t H = 2048, WO = 1792, DO = 257;
+    const int64_t n = H * WO * DO;
+    float* out;
+    if (hipMalloc(&out, n * 4 + 4096) != hipSuccess) return 1;
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    auto time = [&](const char* name, auto launch) {
+        for (int r = 0; r < 30; ++r) launch();  // clocks ramp over the first launches
+        hipDeviceSynchronize();
+        float best = 1e9f;
+        for (int rep = 0; rep < 3; ++rep) {
+            hipEventRecord(a);
+            for (int r = 0; r < 10; ++r) launch();
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms;
+            hipEventElapsedTime(&ms, a, b);
+            ms /= 10;
+            best = ms < best ? ms : best;
+        }
+        printf("%-52s %8.4f ms  %7.1f GB/s\n", name, best, n * 4 / best / 1e6);
+        fflush(stdout);
+    };
+    time("dword grid-stride default", [&] { hipLaunchKernelGGL(k_dword<0>, dim3(8192), dim3(256), 0, 0, out, n); });
+    time("dword grid-stride nt", [&] { hipLaunchKernelGGL(k_dword<2>, dim3(8192), dim3(256), 0, 0, out, n); });
+    time("x4 grid-stride default", [&] { hipLaunchKernelGGL(k_x4<0>, dim3(8192), dim3(256), 0, 0, out, n / 4); });
+    time("x4 grid-stride nt", [&] { hipLaunchKernelGGL(k_x4<2>, dim3(8192), dim3(256), 0, 0, out, n / 4); });
+    char nm[96];
+#define TILE(X4, AUX, BAR, ST, TW, TH, LDS, NAME)                                                           \
+    {                                                                                                       \
+        const int nTile = (int)((WO + TW - 1) / TW), nBand = (int)((H + TH - 1) / TH);                      \
+        snprintf(nm, sizeof nm, "tile%d TH%d lds%dK %s", TW, TH, LDS / 1024, NAME);                       \
+        time(nm, [&] {                                                                                      \
+            hipLaunchKernelGGL((k_tile<X4, AUX, BAR, ST, TW>), dim3(nTile * nBand), dim3(256), LDS, 0, out, H, WO, \
+                               DO, TH, nTile);                                                              \
+        });                                                                                                 \
+    }
+    TILE(true, 2, true, 1, 16, 64, 50000, "x4 nt bar (current)");
+    TILE(true, 0, true, 1, 16, 64, 50000, "x4 default bar");
+    TILE(true, 2, false, 1, 16, 64, 50000, "x4 nt nobar");
+    TILE(false, 2, true, 1, 16, 64, 50000, "dword nt bar");
+    TILE(false, 0, true, 1, 16, 64, 50000, "dword default bar");
+    TILE(true, 2, true, 2, 16, 64, 50000, "x4 nt bar 2 steps/burst");
+    TILE(true, 2, true, 1, 16, 64, 78000, "x4 nt bar 2 WG/CU");
+    TILE(true, 2, true, 1, 16, 64, 38000, "x4 nt bar 4 WG/CU");
+    TILE(true, 2, true, 1, 16, 64, 30000, "x4 nt bar 5 WG/CU");
+    TILE(true, 2, true, 1, 16, 64, 0, "x4 nt bar 8 WG/CU");
+    TILE(false, 2, true, 1, 16, 64, 0, "dword nt bar 8 WG/CU");
+    TILE(true, 2, true, 1, 32, 64, 50000, "x4 nt bar");
+    TILE(true, 2, true, 1, 16, 128, 50000, "x4 nt bar");
+    TILE(true, 2, true, 1, 16, 32, 50000, "x4 nt bar");
+    return 0;
+}

@@ -415,6 +415,39 @@ def test_band_api_matches_whole_image(gpu, layout, D):
     assert float((acc_p - rp).abs().max()) <= 1e-5 * max(1.0, float(rp.abs().max()))
 
 
+@pytest.mark.parametrize("layout,D", [(FULL, 0), (WIN, 12)])
+@pytest.mark.parametrize("k", [7, 6, 11])
+def test_band_forward_reads_only_its_patch_rows(gpu, monkeypatch, layout, D, k):
+    """Volume rows [b, e) of a band depend only on image rows [b - k/2, e + k-1-k/2) and on the
+    statistics of rows [b, e): with every other image row NaN and the workspace filled with NaN,
+    the band's forward (fast and exact) and disparity equal the whole-image results.  This is what
+    lets the row-band forward compute its interior rows while the halo rows are still in flight."""
+    import custereomatching_amd.stereo_matching_wrapper as smw
+    import custereomatching_amd.disparity as disp
+
+    H, W = 48, 64
+    o, a = k // 2, k - 1 - k // 2
+    cam, proj = make_pair(H, W, 16, seed=46)
+    c, p = _dev(cam, gpu), _dev(proj, gpu)
+    ref = {pr: cm.cost_volume_forward(c, p, D, k, layout, pr) for pr in ("fast", "exact")}
+    ri, rb = cm.stereo_disparity(c, p, D, k, layout)
+    nan_ws = lambda nb, dev: torch.full((max(nb, 1) // 4 + 1,), float("nan"), device=dev).view(torch.uint8)
+    monkeypatch.setattr(smw, "_workspace", nan_ws)
+    if hasattr(disp, "_workspace"):
+        monkeypatch.setattr(disp, "_workspace", nan_ws)
+    for b, e in ((0, 9), (13, 30), (40, 48)):
+        cn, pn = c.clone(), p.clone()
+        lo, hi = max(0, b - o), min(H, e + a)
+        for x in (cn, pn):
+            x[:lo] = float("nan")
+            x[hi:] = float("nan")
+        for pr in ("fast", "exact"):
+            vb = cm.cost_volume_forward(cn, pn, D, k, layout, pr, rows=(b, e))
+            assert torch.equal(vb, ref[pr][b:e]), (pr, b, e)
+        ib, bb = cm.stereo_disparity(cn, pn, D, k, layout, rows=(b, e))
+        assert torch.equal(ib, ri[b:e]) and torch.equal(bb, rb[b:e])
+
+
 @pytest.mark.parametrize("layout,D", [(FULL, 0), (WIN, 20)])
 def test_backward_given_volume_matches_recompute(gpu, layout, D):
     """The autograd op hands the forward's volume to the backward (V = g * cost / S); the

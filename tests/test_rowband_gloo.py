@@ -48,7 +48,7 @@ class OracleBackend:
         return torch.from_numpy(idx), torch.from_numpy(best)
 
 
-def _worker(rank, world, port, H, W, k, D, layout, q, pass_h=False):
+def _worker(rank, world, port, H, W, k, D, layout, q, pass_h=False, split=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -56,7 +56,7 @@ def _worker(rank, world, port, H, W, k, D, layout, q, pass_h=False):
         from custereomatching_amd.rowband import band_bounds, stereo_disparity_rowband, stereo_matching_rowband
 
         cam, proj = make_pair(H, W, max(D, 1), seed=17)
-        b, e = band_bounds(H, world, rank)
+        b, e = band_bounds(H, world, rank) if split is None else split[rank]
         c = torch.from_numpy(cam[b:e].copy()).requires_grad_(True)
         p = torch.from_numpy(proj[b:e].copy()).requires_grad_(True)
         be = OracleBackend()
@@ -74,11 +74,12 @@ def _worker(rank, world, port, H, W, k, D, layout, q, pass_h=False):
         dist.destroy_process_group()
 
 
-def _run(world, H, W, k, D, layout, pass_h=False):
+def _run(world, H, W, k, D, layout, pass_h=False, split=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, k, D, layout, q, pass_h)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, k, D, layout, q, pass_h, split))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
@@ -116,6 +117,27 @@ def test_rowband_thin_band_raises_on_every_rank(pass_h):
     before any halo exchange (no rank left waiting in batch_isend_irecv)."""
     res = _run(2, 9, 16, 11, 2, "full", pass_h)
     assert [t[1] for t in res] == ["ValueError", "ValueError"]
+
+
+@pytest.mark.parametrize("pass_h", [False, True])
+def test_rowband_custom_split(pass_h):
+    """A custom row split (3 / 2 / 4 rows of H = 9, not band_bounds's 3 / 3 / 3) at k = 3: with H
+    given, every rank raises (the split check is collective: no rank enters the halo exchange
+    alone); without H the custom split runs and matches the single-device result."""
+    H, W, D, k = 9, 16, 2, 3
+    split = [(0, 3), (3, 5), (5, 9)]
+    res = _run(3, H, W, k, D, "full", pass_h, split)
+    if pass_h:
+        assert [t[1] for t in res] == ["ValueError"] * 3
+        return
+    cam, proj = make_pair(H, W, D, seed=17)
+    vol = O.forward(cam, proj, k, layout=O.FULL, D=0)
+    g = np.random.default_rng(5).standard_normal(O.volume_shape(H, W, O.FULL, 0)).astype(np.float32)
+    rc, _ = O.backward_f64(g, cam, proj, k, layout=O.FULL, D=0)
+    for rank, b, e, v, gc, gp, idx in res:
+        assert (b, e) == split[rank]
+        assert np.array_equal(v, vol[b:e])
+        assert np.abs(gc - rc[b:e]).max() <= 1e-6 * max(1, np.abs(rc).max())
 
 
 def test_band_bounds_partition():

@@ -23,14 +23,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, H, W, k, D, layout, q):
+def _worker(rank, world, port, H, W, k, D, layout, q, backend="gloo"):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = rank if backend == "nccl" else 0  # nccl: one GPU per rank (RCCL over xGMI)
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        torch.cuda.set_device(0)
         from custereomatching_amd.rowband import band_bounds, stereo_disparity_rowband, stereo_matching_rowband
 
         cam, proj = make_pair(H, W, D, seed=41)
@@ -51,15 +55,14 @@ def _worker(rank, world, port, H, W, k, D, layout, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("layout,D,k", [("full", 0, 9), ("window", 48, 11), ("window", 20, 4)])
-def test_rowband_hip_backend_matches_single_device(gpu, layout, D, k):
+def _run_and_compare(gpu, layout, D, k, backend):
     import custereomatching_amd as cm
 
     H, W, world = 70, 160, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, k, D, layout, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, k, D, layout, q, backend)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
@@ -85,3 +88,15 @@ def test_rowband_hip_backend_matches_single_device(gpu, layout, D, k):
         assert np.array_equal(ib, idx[b:e]) and np.array_equal(bb, best[b:e])
         covered += e - b
     assert covered == H
+
+
+@pytest.mark.parametrize("layout,D,k", [("full", 0, 9), ("window", 48, 11), ("window", 20, 4)])
+def test_rowband_hip_backend_matches_single_device(gpu, layout, D, k):
+    _run_and_compare(gpu, layout, D, k, "gloo")
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL over xGMI between them)")
+@pytest.mark.parametrize("layout,D,k", [("full", 0, 9), ("window", 48, 11)])
+def test_rowband_nccl_two_gpus(gpu, layout, D, k):
+    """The transport bench.py uses at N > 1: nccl (RCCL), one rank per GPU, halos device to device."""
+    _run_and_compare(gpu, layout, D, k, "nccl")
