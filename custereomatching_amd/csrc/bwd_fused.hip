@@ -85,16 +85,23 @@ __host__ __device__ inline ChunkGeo chunk_geo(const Geo& g, int64_t dlo, int j) 
         const int64_t b = g.W - c.d0;
         c.whi = b < g.W ? b : g.W;
     }
-    const int64_t span = c.whi - c.wlo + 2 * (int64_t)g.r, n = span > kSeg ? (span + kSeg - 1) / kSeg : 1;
+    const int64_t span = c.whi - c.wlo + (g.k - 1), n = span > kSeg ? (span + kSeg - 1) / kSeg : 1;
     c.seg = span > 0 ? (span + n - 1) / n : 1;
     return c;
 }
-__host__ __device__ inline int chunk_nseg(const ChunkGeo& c, int r) {
-    return (int)((c.whi - c.wlo + 2 * r + c.seg - 1) / c.seg);
+// Taps: the forward's patch of voxel (h, w) covers rows h - r0 .. h + r1 (r0 = k/2, r1 = k-1-k/2, the
+// reference's kernel_size / 2 origin, stereo_matching_kernel.cu:44,60), so an output pixel (y, x) gathers
+// the voxels h in [y - r1, y + r0], w in [x - r1, x + r0] (r0 = r1 = r for odd k).
+struct Taps {
+    int r0, r1;
+};
+__host__ __device__ inline Taps taps_of(const Geo& g) { return Taps{g.k / 2, g.k - 1 - g.k / 2}; }
+__host__ __device__ inline int chunk_nseg(const ChunkGeo& c, Taps t) {
+    return (int)((c.whi - c.wlo + t.r0 + t.r1 + c.seg - 1) / c.seg);
 }
-// Segment s of chunk c: output pixel columns [xs, xe); the sweep runs w in [xs - r, xe + r).
-__host__ __device__ inline void seg_cols(const ChunkGeo& c, int r, int s, int64_t* xs, int64_t* xe) {
-    const int64_t tlo = c.wlo - r, thi = c.whi + r;
+// Segment s of chunk c: output pixel columns [xs, xe); the sweep runs w in [xs - r1, xe + r0).
+__host__ __device__ inline void seg_cols(const ChunkGeo& c, Taps tp, int s, int64_t* xs, int64_t* xe) {
+    const int64_t tlo = c.wlo - tp.r0, thi = c.whi + tp.r1;
     *xs = tlo + (int64_t)s * c.seg;
     const int64_t e = *xs + c.seg;
     *xe = e < thi ? e : thi;
@@ -102,21 +109,21 @@ __host__ __device__ inline void seg_cols(const ChunkGeo& c, int r, int s, int64_
 // Written column range [lo, hi) of partial type t for segment s of chunk c (before clipping
 // to [0, W)).  Camera types: the segment's own columns.  Projector types: every column
 // whose accumulator passed lane 0 during the sweep or sat in the wave at its end.
-__host__ __device__ inline void seg_range(const ChunkGeo& c, int r, int s, int t, int64_t* lo, int64_t* hi) {
+__host__ __device__ inline void seg_range(const ChunkGeo& c, Taps tp, int s, int t, int64_t* lo, int64_t* hi) {
     int64_t xs, xe;
-    seg_cols(c, r, s, &xs, &xe);
-    const int64_t w0 = xs - r, w1 = xe + r;  // sweep steps [w0, w1)
+    seg_cols(c, tp, s, &xs, &xe);
+    const int64_t w0 = xs - tp.r1, w1 = xe + tp.r0;  // sweep steps [w0, w1)
     switch (t) {
         case 0: case 1: case 2: *lo = xs; *hi = xe; break;                                // T1c, Am, B
-        case 3: *lo = w0 - 1 - r + c.d0; *hi = w1 - 1 - r + c.d0 + NLB; break;              // T1p
+        case 3: *lo = w0 - 1 - tp.r0 + c.d0; *hi = w1 - 1 - tp.r0 + c.d0 + NLB; break;      // T1p
         default: *lo = w0 - 1 + c.d0; *hi = w1 - 1 + c.d0 + NLB; break;                     // Ac, Bp
     }
 }
 // Union over the chunk's segments (contiguous).
-__host__ __device__ inline void type_range(const ChunkGeo& c, int r, int t, int64_t* lo, int64_t* hi) {
+__host__ __device__ inline void type_range(const ChunkGeo& c, Taps tp, int t, int64_t* lo, int64_t* hi) {
     int64_t l0, h0, l1, h1;
-    seg_range(c, r, 0, t, &l0, &h0);
-    seg_range(c, r, chunk_nseg(c, r) - 1, t, &l1, &h1);
+    seg_range(c, tp, 0, t, &l0, &h0);
+    seg_range(c, tp, chunk_nseg(c, tp) - 1, t, &l1, &h1);
     *lo = l0;
     *hi = h1;
 }
@@ -224,7 +231,8 @@ template <int K, bool WIN>
 __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, int j, int sg, int rg, float* Abuf,
                                               float* ring, float (*cbuf)[12], float (*pbuf)[12], float* camb) {
     constexpr bool CAML = cam_lds_for<K>();
-    constexpr int R = K / 2, NY = TRB + 2 * R, NH = 2 * R;  // NH halo rows
+    // A rows of the unit: image rows y0 - R1 .. y0 + TRB - 1 + R0 (R1 halo rows above, R0 below)
+    constexpr int R0 = K / 2, R1 = K - 1 - K / 2, NY = TRB + K - 1, NH = K - 1;  // NH halo rows
     constexpr int FBC = fbc_for<K>();
     static_assert(FBC % (BDP + 1) == 0 && FBC <= 16, "flush blocks start on load buffer 0; 4 FBC lanes");
     constexpr int HPW = (NH + NWC - 1) / NWC;                // halo rows per wave (at most)
@@ -238,9 +246,9 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     const int64_t y0 = a.ylo + (int64_t)TRB * rg;
     const int y0i = (int)y0;
     int64_t xs64, xe64;
-    seg_cols(cg, R, sg, &xs64, &xe64);
+    seg_cols(cg, Taps{R0, R1}, sg, &xs64, &xe64);
     const int xs = (int)xs64, xe = (int)xe64;
-    const int w0 = xs - R, wend = xe + R;
+    const int w0 = xs - R1, wend = xe + R0;  // step w completes the horizontal box of output column w - R0
     const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
     int lwlo, lwhi;
     if (window) {
@@ -257,10 +265,10 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 
     const uint32_t ib = (uint32_t)(plane * 4);
     const size_t slab = (size_t)g.WO * g.DO;
-    const int64_t vrow0 = max(g.h_lo, y0 - R);
+    const int64_t vrow0 = max(g.h_lo, y0 - R1);
     const auto rG = make_rsrc(a.grad + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
     const auto rV = make_rsrc(a.vol + (size_t)(vrow0 - g.h_lo) * slab, 0x7FFFFFF0u);
-    const int64_t ir0 = y0 - R;
+    const int64_t ir0 = y0 - R1;
     const uint32_t vstride = (uint32_t)(slab * 4);
     const uint32_t vNR = WIN ? kWinNR : 0x7FFFFFF0u;  // the volume descriptors' num_records
     const int hlo = (int)g.h_lo, hhi = (int)g.h_hi, vrow0i = (int)vrow0;
@@ -310,10 +318,10 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             const int p = 4 * t + m;
-            const int col = wfirst + jcol - (t == 0 ? R : 0);
+            const int col = wfirst + jcol - (t == 0 ? R0 : 0);
             const bool cok = live && col >= xs && col < xe && col >= 0 && col < Wi;
             st_buf(cbuf[jcol][p], part_rsrc(t), cok ? (uint32_t)((m * Wi + col) * 4) : kOOB);
-            const int pcol = wfirst + jcol - 1 + (t == 0 ? -R : 0) + d0;
+            const int pcol = wfirst + jcol - 1 + (t == 0 ? -R0 : 0) + d0;
             const uint32_t poff = (live && pcol >= 0 && pcol < Wi) ? (uint32_t)((m * Wi + pcol) * 4) : kOOB;
             st_buf(pbuf[jcol][p], part_rsrc(3 + t), poff);
         }
@@ -330,7 +338,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     }
 
     // rows of the unit this wave turns into A: its own rows, then its share of the halo
-    auto halo_row = [&](int q) { return q < R ? q : q + TRB; };  // q in [0, 2R)
+    auto halo_row = [&](int q) { return q < R1 ? q : q + TRB; };  // q in [0, K - 1)
     constexpr int HP = HPW > 0 ? HPW : 1;
 
     // ---- loads: issued one step ahead as inline asm (hand-counted waits; the compiler's
@@ -350,8 +358,8 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     uint32_t sIo[TRW], sVo[TRW], sIh[HP], sVh[HP];
 #pragma unroll
     for (int m = 0; m < TRW; ++m) {
-        sIo[m] = __builtin_amdgcn_readfirstlane(iso(R + yw + m));
-        sVo[m] = __builtin_amdgcn_readfirstlane(vso(R + yw + m));
+        sIo[m] = __builtin_amdgcn_readfirstlane(iso(R1 + yw + m));
+        sVo[m] = __builtin_amdgcn_readfirstlane(vso(R1 + yw + m));
     }
 #pragma unroll
     for (int i = 0; i < HP; ++i) {
@@ -389,7 +397,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     const uint32_t gsU4 = (uint32_t)gsU * 4u;
     auto issue = [&](int w, Ld& b, auto nop_) {
         constexpr bool NOP = decltype(nop_)::value;
-        const int xb = w - R;
+        const int xb = w - R0;
         if constexpr (WIN) {
             // wave-uniform parts: the step's volume column (marker outside [0, WO)) and the two
             // camera columns w and w - R (marker outside [0, W))
@@ -418,7 +426,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     // sc[3m + {0, 1, 2}] = Y, mp', p' of own row m; bc the same for the block
     uint32_t sc[3 * TRW], shY[HP], bc[3 * TRW], bhY[HP];
     auto load_cols = [&](uint32_t* c, uint32_t* hY, int cb) {
-        const uint32_t oY = col_off_a(cb + dl, kY), oM = col_off_a(cb + dl, kMp), oP = col_off_a(cb - R + dl, kP);
+        const uint32_t oY = col_off_a(cb + dl, kY), oM = col_off_a(cb + dl, kMp), oP = col_off_a(cb - R0 + dl, kP);
 #pragma unroll
         for (int m = 0; m < TRW; ++m) {
             asm_ld2s(c[3 * m], c[3 * m + 1], oY, oM, dPr, dPr, sIo[m], sIo[m]);
@@ -433,7 +441,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     uint32_t cbk[NCB];
     auto load_cam = [&](int wb) {
         if constexpr (CAML) {
-            const uint32_t oX = col_off_a(wb + lane, kX), oM = col_off_a(wb + lane, kMc), oC = col_off_a(wb - R + lane, kC);
+            const uint32_t oX = col_off_a(wb + lane, kX), oM = col_off_a(wb + lane, kMc), oC = col_off_a(wb - R0 + lane, kC);
 #pragma unroll
             for (int m = 0; m < TRW; ++m) {
                 asm_ld2s(cbk[3 * m], cbk[3 * m + 1], oX, oM, dPr, dPr, sIo[m], sIo[m]);
@@ -538,7 +546,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             for (int t = 0; t < 3; ++t)
                 *(float4*)&pbuf[s][4 * t] = make_float4(P[t][0], P[t][1], P[t][2], P[t][3]);
         }
-        const int xb = w - R;
+        const int xb = w - R0;
         const float tf = xb >= xs ? 1.f : 0.f, af = (w >= xs && w < xe) ? 1.f : 0.f;
         const float mco = F(cmc_r) * af;
         const float cxo = (F(ccx_r) - cb) * tf;
@@ -547,7 +555,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         float amv[TRW], bv[TRW];
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
-            const int y = R + yw + m;
+            const int y = R1 + yw + m;
             const float Xf = rbc<m>(F(cxo_r)), Ye = F(sc[3 * m]);
             const float rSe = __builtin_amdgcn_rsqf(__builtin_fmaf(Xf, Ye, kEps));
             const float Ae = F(cur.ge[m]) * rSe;
@@ -570,14 +578,14 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         if (s > 0) reduce_to(s - 1);
         __syncthreads();  // the unit's A rows of this step are published
         // ---- vertical k-row sums of own rows, horizontal slide through the ring ----
-        float col[TRW + 2 * R];
+        float col[TRW + K - 1];
 #pragma unroll
-        for (int y = 0; y < TRW + 2 * R; ++y) col[y] = Acur[(yw + y) * 64 + lane];
-        float v = tree_sum<2 * R + 1>(col);  // a pairwise tree: depth log2(k) instead of a k-long chain
+        for (int y = 0; y < TRW + K - 1; ++y) col[y] = Acur[(yw + y) * 64 + lane];
+        float v = tree_sum<K>(col);  // a pairwise tree: depth log2(k) instead of a k-long chain
         float t1v[TRW];
         Unroll<0, TRW>::run([&](auto mi) {
             constexpr int m = decltype(mi)::value;
-            if (m > 0) v = (v + col[m + 2 * R]) - col[m - 1];
+            if (m > 0) v = (v + col[m + K - 1]) - col[m - 1];
             HV[m] += v - rsv[m];
             ring[(sidx * TRW + m) * 64 + lane] = v;
             t1v[m] = (F(sc[3 * m + 2]) - pb) * HV[m];  // p'(row, xb + dl) BoxA
@@ -627,7 +635,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     // ---- final projector state: lane l holds column (wend - 1) + off + d0 + l
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
-        const int col = wend - 1 + (t == 0 ? -R : 0) + d0 + lane;
+        const int col = wend - 1 + (t == 0 ? -R0 : 0) + d0 + lane;
         const uint32_t c4 = (col >= 0 && col < g.W) ? (uint32_t)(col * 4) : kOOB;
         const auto rp = part_rsrc(3 + t);
 #pragma unroll
@@ -830,14 +838,14 @@ __global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
         j = chunk_of_rank(jr, a.nChunk, a.jc);
         sg = (int)(unit / nU);
     }
-    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), g.r)) return;
-    constexpr int NY = TRB + 2 * (K / 2);
+    if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), taps_of(g))) return;
+    constexpr int NY = TRB + K - 1;
     __shared__ __attribute__((aligned(16))) float Abuf[2 * NY * 64];
     __shared__ __attribute__((aligned(16))) float ring[NWC * K * TRW * 64];
     constexpr int FBC = fbc_for<K>();
     __shared__ __attribute__((aligned(16))) float cbuf[NWC][FBC][12];
     __shared__ __attribute__((aligned(16))) float pbuf[NWC][FBC][12];
-    constexpr int HPW = (2 * (K / 2) + NWC - 1) / NWC;
+    constexpr int HPW = (K - 1 + NWC - 1) / NWC;
     __shared__ float camL[NWC][cam_lds_for<K>() ? (12 + (HPW > 0 ? HPW : 1)) * kCamP : 1];
     const int wv = threadIdx.x >> 6;
     bwd_coop_body<K, WIN>(g, a, j, sg, rg, Abuf, ring + wv * (K * TRW * 64), cbuf[wv], pbuf[wv], camL[wv]);
@@ -857,19 +865,20 @@ __host__ __device__ inline int cover_column(const Geo& g, int64_t dlo, int nChun
     for (int j = 0; j < nChunk; ++j) {
         const ChunkGeo c = chunk_geo(g, dlo, j);
         int64_t lo, hi;
-        type_range(c, g.r, t, &lo, &hi);
+        type_range(c, taps_of(g), t, &lo, &hi);
         if (x < lo || x >= hi) continue;
-        const int ns = chunk_nseg(c, g.r);
+        const int ns = chunk_nseg(c, taps_of(g));
         // the segment(s) of chunk j whose written range holds column x (<= 2, adjacent)
-        const int64_t rel = x - (c.wlo - g.r) - (cls ? c.d0 : 0);
+        const Taps tp = taps_of(g);
+        const int64_t rel = x - (c.wlo - tp.r0) - (cls ? c.d0 : 0);
         // segments whose written range can hold x: relative to segment s's own first column
-        // s seg, every range lies in [-2r - 1, seg + r + 63) (seg_range); checked exactly below
+        // s seg, every range lies in [-k, seg + r0 + 63) (seg_range); checked exactly below
         auto fdiv = [](int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
-        const int s_lo = (int)fdiv(rel - c.seg - g.r - NLB, c.seg);
-        const int s_hi = (int)fdiv(rel + 2 * g.r + 1, c.seg);
+        const int s_lo = (int)fdiv(rel - c.seg - tp.r0 - NLB, c.seg);
+        const int s_hi = (int)fdiv(rel + g.k, c.seg);
         for (int sg = s_lo < 0 ? 0 : s_lo; sg <= s_hi; ++sg) {
             if (sg < 0 || sg >= ns) continue;
-            seg_range(c, g.r, sg, t, &lo, &hi);
+            seg_range(c, tp, sg, t, &lo, &hi);
             if (x >= lo && x < hi) {
                 if (list && n < S) list[n] = (unsigned short)(2 * (j % Sj) + (sg & 1));
                 ++n;
@@ -914,7 +923,7 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
         if (q == 0) {
             // written for camera columns x < WO + r (past them the box of diagonal D is empty) and
             // projector columns o >= D - r
-            if (side == 0 ? x < g.WO + g.r : x >= D - g.r) s += (double)remT1[side * nyw + yy * g.W + x];
+            if (side == 0 ? x < g.WO + (g.k - 1 - g.r) : x >= D - g.r) s += (double)remT1[side * nyw + yy * g.W + x];
         } else {
             const int64_t w = side == 0 ? x : x - D;  // the voxel column of this pixel on diagonal D
             if (y >= g.h_lo && y < g.h_hi && w >= 0 && w < g.WO)
@@ -974,7 +983,9 @@ __global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict
     const acc_t* T1 = acc + (size_t)side * 3 * plane;
     const acc_t* Zz = T1 + plane;
     const acc_t* Bb = Zz + plane;
-    const int k = KT > 0 ? KT : g.k, r = k / 2, L = TS + 2 * r;
+    // Box over rows y - r1 .. y + r0 and columns x - r1 .. x + r0 (r1 = k-1-k/2: the transpose of the forward's
+    // patch); the tile's inputs start r1 rows / columns before the outputs
+    const int k = KT > 0 ? KT : g.k, r = k - 1 - k / 2, L = TS + k - 1;
     double* hZ = tl;                 // [L][TS] row sums
     double* hB = hZ + L * TS;
     float* tZ = (float*)(hB + L * TS);  // [L][L] inputs
@@ -1086,7 +1097,7 @@ struct BwdPlan {
 // reads (+ one row of columns and diagonals), and the six prepared images.
 bool win_path_ok(const Geo& g) {
     const double slab = (double)g.WO * (double)g.DO * 4.0;
-    return g.layout == CUSTMA_LAYOUT_WINDOW && slab * (TRB + 2 * g.r + 2) < (double)kWinNR &&
+    return g.layout == CUSTMA_LAYOUT_WINDOW && slab * (TRB + g.k + 1) < (double)kWinNR &&
            (double)g.H * (double)g.W * 24.0 < (double)kWinNR;
 }
 
@@ -1118,7 +1129,7 @@ BwdPlan plan_bwd(const Geo& g) {
 
 BwdPlan plan_bwd_uncached(const Geo& g) {
     BwdPlan p;
-    const int r = g.r;
+    const Taps tp = taps_of(g);
     p.rem = false;
     if (g.layout == CUSTMA_LAYOUT_WINDOW) {
         p.dlo = 0;
@@ -1126,7 +1137,7 @@ BwdPlan plan_bwd_uncached(const Geo& g) {
         p.jc = 0;
         // D = 64 n: the last diagonal alone would take a fifth chunk of sweeps with one live lane
         // in 64; k_bwd_rem_rows takes it instead (the window form only)
-        if (g.D >= NLB && (g.D + 1) % NLB == 1 && win_path_ok(g)) {
+        if (g.D >= NLB && (g.D + 1) % NLB == 1 && win_path_ok(g) && g.k % 2 == 1) {
             p.rem = true;
             p.nChunk -= 1;
         }
@@ -1151,7 +1162,7 @@ BwdPlan plan_bwd_uncached(const Geo& g) {
             ev.clear();
             for (int j = 0; j < p.nChunk; ++j) {
                 int64_t lo, hi;
-                type_range(chunk_geo(g, p.dlo, j), r, ts[c], &lo, &hi);
+                type_range(chunk_geo(g, p.dlo, j), tp, ts[c], &lo, &hi);
                 lo = lo < 0 ? 0 : lo;
                 hi = hi > W ? W : hi;
                 if (lo < hi) { ev.emplace_back(lo, 1); ev.emplace_back(hi, -1); }
@@ -1173,11 +1184,12 @@ BwdPlan plan_bwd_uncached(const Geo& g) {
     p.S = 2 * p.Sj;
     p.nsegMax = 1;
     for (int j = 0; j < p.nChunk; ++j) {
-        const int ns = chunk_nseg(chunk_geo(g, p.dlo, j), r);
+        const int ns = chunk_nseg(chunk_geo(g, p.dlo, j), tp);
         if (ns > p.nsegMax) p.nsegMax = ns;
     }
-    p.ylo = g.h_lo - r > 0 ? g.h_lo - r : 0;
-    p.yhi = g.h_hi + r < g.H ? g.h_hi + r : g.H;
+    // gradient rows: voxel row h feeds output rows h - r0 .. h + r1
+    p.ylo = g.h_lo - tp.r0 > 0 ? g.h_lo - tp.r0 : 0;
+    p.yhi = g.h_hi + tp.r1 < g.H ? g.h_hi + tp.r1 : g.H;
     p.nRG = (int)cdiv(p.yhi - p.ylo, TRB);
     const size_t plane = (size_t)g.H * g.W;
     p.part_bytes = (size_t)NTYPE * p.S * plane * sizeof(float);
@@ -1276,7 +1288,7 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
                        a.remT, a.remT1);
     {
         constexpr int TS3 = 32;
-        const int L3 = TS3 + 2 * g.r;
+        const int L3 = TS3 + g.k - 1;
         const size_t lds3 = sizeof(double) * 2 * L3 * TS3 + sizeof(float) * 2 * L3 * L3;
         const dim3 cgrid((unsigned)cdiv(g.W, TS3), (unsigned)cdiv(g.H, TS3), 2);
         auto go = [&](auto kc) {
@@ -1312,7 +1324,7 @@ bool backward_supported(const Geo& g) {
     // image must stay below 2 GiB
     if (!plan_bwd(g).ok) return false;
     const double slab = (double)g.WO * (double)g.DO * 4.0;
-    return slab * (TRB + 2 * g.r + 1) < 2147483648.0 && (double)g.H * (double)g.W * 8.0 < 2147483648.0;
+    return slab * (TRB + g.k) < 2147483648.0 && (double)g.H * (double)g.W * 8.0 < 2147483648.0;
 }
 
 hipError_t launch_backward(const float* grad, const float* vol, const void* cam, const void* proj, int dtype,

@@ -98,7 +98,7 @@ __device__ __forceinline__ void fin_bc(double& e, float& den2, double s, double 
 // Kernel sizes with a compile-time sweep instantiation (register-resident
 // column sums need a static trip count).  Other odd sizes up to
 // CUSTMA_MAX_KERNEL run on the exact kernel.
-#define CUSTMA_SWEEP_KS(X) X(1) X(3) X(5) X(7) X(9) X(11) X(13) X(15) X(17)
+#define CUSTMA_SWEEP_KS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17)
 
 struct SweepGrid {
     int nChunk;  // diagonal chunks per column tile

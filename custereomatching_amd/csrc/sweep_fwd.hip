@@ -49,7 +49,9 @@ template <int K, int TWT, typename T, bool ARGMAX>
 __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                    Stats sc, Stats sp, float* __restrict__ out, SweepGrid sg,
                                                    DispPartial part) {
-    constexpr int R = K / 2, NX = TWT + 2 * R;
+    // taps rows h - R0 .. h + R1, columns w - R0 .. w + R1 (R0 = K/2, R1 = K-1-K/2: the reference's
+    // kernel_size / 2 origin, stereo_matching_kernel.cu:44,60)
+    constexpr int R0 = K / 2, R1 = K - 1 - K / 2, NX = TWT + K - 1;
     static_assert(TWT == 16 && NX <= 32, "row-broadcast layout assumes 16 own columns and <= 32 taps");
     constexpr int NL_MAX = 320, LO = (NX + NL_MAX - 1 + 63) / 64, LS = (TWT + NL_MAX - 1 + 63) / 64;
     const int NL = sg.NL, NO = NX + NL - 1, NS = TWT + NL - 1;
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     const int band = (int)(rest / sg.nTile);
     const int64_t u0 = (int64_t)wt * TWT;
     const int64_t h0 = g.h_lo + (int64_t)band * sg.TH, h1 = min(g.h_hi, h0 + sg.TH);
-    const int64_t hs = h0 - 2 * R;  // first step: 2R warm-up steps fill the column sums
+    const int64_t hs = h0 - (K - 1);  // first step: K - 1 warm-up steps fill the column sums
     const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
     const int64_t dlo = window ? 0 : -(u0 + TWT - 1);
     const int64_t dhi = window ? g.D : g.W - 1 - u0;
@@ -92,7 +94,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         // padding, stereo_matching_kernel.cu:6-12): loop-invariant per-lane byte offsets,
         // the row chosen by the descriptor (zero-size for rows outside the image) ----
         const int li = tid - NL;
-        const int64_t xU0 = u0 - R, xO0 = u0 - R + d0, oS = u0 + d0;
+        const int64_t xU0 = u0 - R0, xO0 = u0 - R0 + d0, oS = u0 + d0;
         auto colOff = [&](bool have, int64_t x, int esz) -> uint32_t {
             return (have && x >= 0 && x < g.W) ? (uint32_t)(x * esz) : OOB;
         };
@@ -119,12 +121,12 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             uint32_t ue, ul, oe[LO], ol[LO], q[LS], uq;
             double m[LS], ub;
         };
-        // step t adds image row t+R and removes row t-R-1 (once it was added: rows from
-        // h0-R on are added, so the first removal is at t = h0+1)
+        // step t adds image row t+R1 and removes row t-R0-1 (once it was added: rows from
+        // h0-R0 on are added, so the first removal is at t = h0+1)
         auto load_step = [&](int64_t t, Stage& p) {
             const bool rem = t > h0;
-            const auto rCe = row_rsrc(cam, t + R, sizeof(T), true), rCl = row_rsrc(cam, t - R - 1, sizeof(T), rem);
-            const auto rPe = row_rsrc(proj, t + R, sizeof(T), true), rPl = row_rsrc(proj, t - R - 1, sizeof(T), rem);
+            const auto rCe = row_rsrc(cam, t + R1, sizeof(T), true), rCl = row_rsrc(cam, t - R0 - 1, sizeof(T), rem);
+            const auto rPe = row_rsrc(proj, t + R1, sizeof(T), true), rPl = row_rsrc(proj, t - R0 - 1, sizeof(T), rem);
             asm_ld_raw<T>(p.ue, vUe, rCe);
             asm_ld_raw<T>(p.ul, vUl, rCl);
 #pragma unroll
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         if (h >= h0) {
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
 #pragma unroll
-            for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
+            for (int x = 1; x < K; ++x) s += col[x];
             const lds_vd* mrow = (const lds_vd*)(rsM + buf * SP + tid);
             const float* qrow = rsQ + buf * SP + tid;
             const double nb = usB[buf * 64 + r16];  // -(camera patch sum) of column r16
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             float* srow = stg + (ARGMAX ? 0 : buf * 16 * NL) + tid;
             Unroll<0, TWT>::run([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
-                if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
+                if (m > 0) s = (s + col[m + K - 1]) - col[m - 1];
                 double e = s;
                 fmac_bc64<m>(e, nb, mv[m]);                 // E + eps = S + eps - box_c * mean_p
                 float den2 = kEps;
@@ -417,7 +419,7 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
     // (per-lane 256-byte stores straight from registers, one chunk of all D+1 diagonals of a window,
     // measured slower: 2.56 vs 2.34 ms at 2048^2, D = 256, k = 11)
     const SweepGrid sg = sweep_grid(g, /*owned=*/part == nullptr);
-    constexpr int R = K / 2, NX = TW + 2 * R;
+    constexpr int NX = TW + K - 1;
     constexpr int NL_MAX = 320, OP = 64 * ((NX + NL_MAX - 1 + 63) / 64), SP = 64 * ((TW + NL_MAX - 1 + 63) / 64);
     const int NL = sg.NL;
     const size_t lds = sizeof(double) * (4 * OP + 2 * 64 + 2 * SP + 2 * 64) +

@@ -66,7 +66,10 @@ constexpr int kFwdPF = 2;  // outputs whose projector statistics are read ahead 
 // index of best), AMX passes of 4 rows per wave, and writes them as one disparity partial.
 // AMX < 0: fused disparity with the soft-argmax sums (DispPartial::s0 / s1), -AMX passes.
 //
-// CPL (STAGED): the workgroup's camera rows h0 - R .. h1 + R - 1, columns u0 - R .. u0 - R + NX - 1
+// Taps (the reference's `kernel_size / 2` origin, stereo_matching_kernel.cu:44,60): rows h - R0 .. h + R1
+// and columns w - R0 .. w + R1 with R0 = K/2, R1 = K-1-K/2 (R0 = R1 = r for odd K; even K is asymmetric).
+//
+// CPL (STAGED): the workgroup's camera rows h0 - R0 .. h1 + R1 - 1, columns u0 - R0 .. u0 - R0 + NX - 1
 // (every wave needs the same ones) are loaded once into LDS (camL, zero-padded) before the sweep,
 // instead of four 16-address loads per wave and step: those loads were most of the sweep's load
 // cost (C5: 9.80 -> 8.25 ms with every camera load out of range, profiles/r03/fwdabl).
@@ -82,13 +85,13 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     typedef std::conditional_t<sizeof(T) == 2, unsigned short, uint32_t> RawT;  // raw image bits
     constexpr int AMX = AMX_ < 0 ? -AMX_ : AMX_;
     constexpr bool SOFT = AMX_ < 0;
-    constexpr int R = K / 2, NX = TW + 2 * R;
+    constexpr int R0 = K / 2, R1 = K - 1 - K / 2, NX = TW + K - 1;
     static_assert(NX + 63 <= kRowP && NX <= 32, "row segment fits the LDS slice and two broadcast registers");
     constexpr uint32_t OOB = 0x80000000u;
     // SS (STAGED): dword stores per thread per step, the same for every wave of the workgroup;
     // SS < 0: -SS 16-byte stores + one dword store (the block's < 4-float tail) per thread
     const int l = threadIdx.x & 63, r16 = l & 15;
-    const int64_t hs = h0 - 2 * R;  // 2R warm-up steps fill the column sums
+    const int64_t hs = h0 - (K - 1);  // K - 1 warm-up steps fill the column sums
     const bool window = g.layout == CUSTMA_LAYOUT_WINDOW;
     const double rk2 = 1.0 / (double)(K * K);
 
@@ -97,9 +100,9 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     auto colOff = [&](bool have, int64_t x, int esz) -> uint32_t {
         return (have && x >= 0 && x < g.W) ? (uint32_t)(x * esz) : OOB;
     };
-    const int64_t xO0 = u0 - R + d0, oS = u0 + d0;
+    const int64_t xO0 = u0 - R0 + d0, oS = u0 + d0;
     const uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 64, xO0 + 64 + l, sizeof(T));
-    const uint32_t vC0 = colOff(true, u0 - R + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R + 16 + r16, sizeof(T));
+    const uint32_t vC0 = colOff(true, u0 - R0 + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R0 + 16 + r16, sizeof(T));
     const uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 64, oS + 64 + l, 8);
     const uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 64, oS + 64 + l, 4);
     const uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
@@ -109,7 +112,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     // column offset is OOB itself (0x80000000 + OOBS does not wrap).
     constexpr uint32_t OOBS = 0x7FFFFFF0u;
     const int Hi = (int)g.H, h0i = (int)h0, h1i = (int)h1;
-    const int rb = max(0, h0i - 3 * R - 1);
+    const int rb = max(0, h0i - 3 * R0 - 1);  // <= the first consumed row h0 - R0
     const uint32_t rbT = (uint32_t)(g.W * sizeof(T)), rb8 = (uint32_t)(g.W * 8), rb4 = (uint32_t)(g.W * 4);
     auto band_rsrc = [&](const void* base, uint32_t rowbytes) {
         const uint64_t n = (uint64_t)(g.H - rb) * rowbytes;
@@ -131,21 +134,21 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     };
     constexpr int kLoads = CPL ? 10 : 14;
     if constexpr (CPL) {
-        // camera rows h0 - R + i (i < h1 - h0 + 2R), columns u0 - R + j (j < NX), raw, 0 outside the image
+        // camera rows h0 - R0 + i (i < h1 - h0 + K - 1), columns u0 - R0 + j (j < NX), raw, 0 outside the image
         typedef __attribute__((address_space(3))) RawT lds_t;
         const RawT* cr = (const RawT*)cam;
-        const int nr = (int)(h1 - h0) + 2 * R;
+        const int nr = (int)(h1 - h0) + K - 1;
         for (int e = (int)threadIdx.x; e < nr * NX; e += (int)blockDim.x) {
-            const int64_t row = h0 - R + e / NX, c = u0 - R + e % NX;
+            const int64_t row = h0 - R0 + e / NX, c = u0 - R0 + e % NX;
             ((lds_t*)camL)[e] = (row >= 0 && row < g.H && c >= 0 && c < g.W) ? cr[row * g.W + c] : (RawT)0;
         }
         __syncthreads();
     }
-    // step t adds image row t+R and removes row t-R-1 (rows from h0-R on were added, so the
+    // step t adds image row t+R1 and removes row t-R0-1 (rows from h0-R0 on were added, so the
     // first removal is at t = h0+1); statistics of row t (only for t in [h0, h1))
     auto load_step = [&](int64_t t, Stage& p) {
         const int ti = (int)t;
-        const uint32_t sE = so_row(ti + R, rbT, true), sL = so_row(ti - R - 1, rbT, ti > h0i);
+        const uint32_t sE = so_row(ti + R1, rbT, true), sL = so_row(ti - R0 - 1, rbT, ti > h0i);
         if constexpr (CPL)
             asm_ld_img4<T>(p.pe0, p.pe1, p.pl0, p.pl1, vP0, vP1, dProj, sE, sL);
         else
@@ -212,10 +215,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         sQ[64 + l] = __builtin_bit_cast(float, p.q1);
         uint32_t ce0 = p.ce0, ce1 = p.ce1, cl0 = p.cl0, cl1 = p.cl1;
         if constexpr (CPL) {
-            // the rows enter t + R and leave t - R - 1 (from t = h0 + 1 on) of the preloaded block
+            // the rows enter t + R1 and leave t - R0 - 1 (from t = h0 + 1 on) of the preloaded block
             typedef __attribute__((address_space(3))) const RawT lds_ct;
             const lds_ct* cr = (const lds_ct*)camL;
-            const int er = (int)(t - h0) + 2 * R, lr = (int)(t - h0) - 1;
+            const int er = (int)(t - h0) + K - 1, lr = (int)(t - h0) - 1;
             const bool hi = 16 + r16 < NX, lv = t > h0;
             ce0 = (uint32_t)cr[er * NX + r16];
             ce1 = hi ? (uint32_t)cr[er * NX + 16 + r16] : 0u;
@@ -266,7 +269,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         }
 
         if constexpr (REM) {
-            const double cRe = l < 16 ? ca0 : ca1, cRl = l < 16 ? cb0 : cb1;  // camera column u0 - R + l
+            const double cRe = l < 16 ? ca0 : ca1, cRl = l < 16 ? cb0 : cb1;  // camera column u0 - R0 + l
             colR = __builtin_fma(cRe, *(const lds_vd*)(rowE + 64 + l), colR);
             colR = __builtin_fma(cRl, *(const lds_vd*)(rowL + 64 + l), colR);
         }
@@ -275,7 +278,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             orow += ostep;
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
 #pragma unroll
-            for (int x = 1; x < 2 * R + 1; ++x) s += col[x];
+            for (int x = 1; x < K; ++x) s += col[x];
             // the projector mean / moment of output m, read PF outputs ahead (plain reads, issued
             // in program order before the stage writes of the outputs in between)
             typedef __attribute__((address_space(3))) const double lds_d;
@@ -299,7 +302,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             constexpr bool MASKED = decltype(masked_c)::value;
             Unroll<0, TW>::run([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
-                if (m > 0) s = (s + col[m + 2 * R]) - col[m - 1];
+                if (m > 0) s = (s + col[m + K - 1]) - col[m - 1];
                 double e;
                 float den2;
                 const double mv = mq[m % PF];
@@ -326,12 +329,12 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             if (!STAGED || allv) outputs(std::false_type{});
             else outputs(std::true_type{});
             if constexpr (REM) {
-                // diagonal D for tile row m = lane: box over the column sums of lanes m .. m + 2R
+                // diagonal D for tile row m = lane: box over the column sums of lanes m .. m + K - 1
                 sR[l] = colR;
                 double sr = (double)kEps;
                 const lds_vd* rr = (const lds_vd*)(sR + (l & 15));
 #pragma unroll
-                for (int x = 0; x < 2 * R + 1; ++x) sr += rr[x];
+                for (int x = 0; x < K; ++x) sr += rr[x];
                 const double e = __builtin_fma(nb, *(const lds_vd*)(sM + 64 + (l & 15)), sr);
                 const float den2 = __builtin_fmaf(uq, *(const lds_vf*)(sQ + 64 + (l & 15)), kEps);
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
@@ -527,8 +530,8 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
 // disparity keeps its per-step camera loads (3 % slower with the preload).
 template <int K, typename T>
 size_t cpl_bytes(const WaveGrid& wg) {
-    constexpr int R = K / 2, NX = TW + 2 * R;
-    return ((size_t)(wg.TH + 2 * R) * NX * sizeof(T) + 15) & ~(size_t)15;
+    constexpr int NX = TW + K - 1;
+    return ((size_t)(wg.TH + K - 1) * NX * sizeof(T) + 15) & ~(size_t)15;
 }
 template <int K, typename T>
 bool cpl_ok(const Geo& g, const WaveGrid& wg, size_t lds) {

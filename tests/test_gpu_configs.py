@@ -139,13 +139,13 @@ def test_config2_forward_backward_full_size(gpu, layout, D):
         assert _rel(p.grad[h0:h1].cpu().numpy(), rp) <= 1e-5
 
 
-# ---------------- generic fp64 backward (even k, odd k > 17) at a mid size ----------------
+# ---------------- k > 17 (generic fp64 backward) and even k (fused sweep) at a mid size ----------------
 
-@pytest.mark.parametrize("layout,D,k", [("window", 64, 16), ("full", 0, 19)])
+@pytest.mark.parametrize("layout,D,k", [("window", 64, 18), ("full", 0, 19), ("window", 64, 16), ("full", 0, 12)])
 def test_generic_backward_mid_size(gpu, layout, D, k):
-    """Mid-size problems through the banded generic backward (grid-stride kernels, bounded workspace;
-    the 512 x 512 full layout takes two bands of output rows at the default 2 GiB band budget),
-    checked on haloed oracle bands."""
+    """Mid-size problems: k > 17 through the banded generic backward (grid-stride kernels, bounded
+    workspace; the 512 x 512 full layout takes two bands of output rows at the default 2 GiB band
+    budget), even k <= 16 through the fused sweep; checked on haloed oracle bands."""
     H = W = 1024 if layout == "window" else 512
     o = k // 2
     cam, proj = make_pair(H, W, max(D, 1), seed=85)
@@ -232,9 +232,9 @@ def test_config4_window_fp16_one_gpu(gpu):
 
 # ---------------- kernel sizes beyond the fused instantiations (generic paths) ----------------
 
-@pytest.mark.parametrize("k", [19, 25, 4, 8])
+@pytest.mark.parametrize("k", [19, 25, 18, 20])
 def test_large_and_even_kernel_sizes_through_autograd(gpu, k):
-    """k = 19, 25 (odd, above the fused backward's 17) and even k (the reference's
+    """k = 19, 25, 18, 20 (above the sliding instantiations; even k with the reference's
     kernel_size / 2 origin): exact forward + generic fp64 backward via the op."""
     H, W, D = 28, 60, 12
     cam, proj = make_pair(H, W, D, seed=200 + k)
@@ -246,6 +246,30 @@ def test_large_and_even_kernel_sizes_through_autograd(gpu, k):
         ref = O.forward(cam, proj, k, layout=lay, D=Dl)
         got = vol.detach().cpu().numpy()
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))  # exact path for these k
+        g = np.random.default_rng(k).standard_normal(ref.shape).astype(np.float32)
+        vol.backward(_dev(g, gpu))
+        rc, rp = O.backward_f64(g, cam, proj, k, layout=lay, D=Dl)
+        assert _rel(c.grad.cpu().numpy(), rc) <= 1e-5
+        assert _rel(p.grad.cpu().numpy(), rp) <= 1e-5
+        idx, best = cm.stereo_disparity(c.detach(), p.detach(), D, k, layout)
+        ridx, _ = O.argmax(ref)
+        assert np.array_equal(idx.cpu().numpy(), ridx)
+
+
+@pytest.mark.parametrize("k", [2, 4, 8, 16])
+def test_even_kernel_sizes_sliding_through_autograd(gpu, k):
+    """Even k (taps -k/2 .. k/2-1, stereo_matching_kernel.cu:44,60) through the sliding kernels:
+    fast forward within the cost bound, fused backward of both images within 1e-5, certified
+    disparity bit-identical to the exact volume's argmax."""
+    H, W, D = 30, 72, 14
+    cam, proj = make_pair(H, W, D, seed=300 + k)
+    for layout in ("full", "window"):
+        c = _dev(cam, gpu).requires_grad_(True)
+        p = _dev(proj, gpu).requires_grad_(True)
+        vol = cm.stereo_matching(c, p, D, k, layout, "fast")
+        lay, Dl = (O.FULL, 0) if layout == "full" else (O.WINDOW, D)
+        ref = O.forward(cam, proj, k, layout=lay, D=Dl)
+        assert np.abs(vol.detach().cpu().numpy() - ref).max() <= O.fast_tolerance(k)
         g = np.random.default_rng(k).standard_normal(ref.shape).astype(np.float32)
         vol.backward(_dev(g, gpu))
         rc, rp = O.backward_f64(g, cam, proj, k, layout=lay, D=Dl)

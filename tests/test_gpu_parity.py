@@ -49,8 +49,11 @@ CASES = [
     (26, 40, 5, 39, "textured"),
     (19, 37, 21, 9, "textured"),  # beyond the sweep instantiations: exact kernel only
     (30, 70, 17, 31, "textured"),  # the largest sweep instantiation (16 + 2r = 32 columns)
-    (20, 44, 4, 9, "textured"),   # even k: taps at -k/2 .. k/2-1 (reference .cu:44,60), exact kernel
+    (20, 44, 4, 9, "textured"),   # even k: taps at -k/2 .. k/2-1 (reference .cu:44,60), sliding kernels
     (17, 33, 10, 6, "smooth"),
+    (21, 50, 2, 11, "textured"),
+    (26, 70, 16, 24, "quantized"),  # the largest even sliding instantiation (16 + 15 = 31 columns)
+    (19, 45, 18, 9, "textured"),   # even k beyond the sliding instantiations: exact kernel only
     (12, 70, 33, 20, "textured"),  # above the old limit of 31
     (24, 48, 5, 16, "constant"),
     (24, 48, 5, 16, "zeros"),
@@ -93,6 +96,8 @@ REM_CASES = [
     (20, 200, 9, 128, torch.float32),
     (18, 300, 11, 256, torch.float16),
     (19, 90, 15, 64, torch.float32),
+    (22, 150, 6, 64, torch.float32),    # even k
+    (17, 300, 16, 256, torch.float16),
 ]
 
 
@@ -160,7 +165,9 @@ DISP_CASES = [
     (24, 48, 5, 16, "zeros"),
     (20, 40, 19, 12, "textured"),  # no sweep instance: every pixel decided exactly
     (24, 64, 17, 20, "textured"),  # the largest sweep instance
-    (20, 40, 4, 12, "textured"),   # even k, likewise
+    (20, 40, 4, 12, "textured"),   # even k (sliding kernels)
+    (22, 70, 16, 20, "quantized"),
+    (20, 40, 18, 12, "textured"),  # even k beyond the sliding instantiations: decided exactly
 ]
 
 
@@ -226,12 +233,17 @@ BWD_CASES = [
     # k = 17: the largest fused instantiation (one workgroup per CU: 92 KB of LDS)
     (26, 80, 17, 20, "textured"),
     (20, 140, 17, 64, "smooth"),
-    # generic fp64 backward (no fused instantiation): odd k > 17 and even k
-    (20, 44, 19, 9, "textured"),
-    (16, 40, 25, 12, "smooth"),
+    # even k on the fused sweep: rows / columns y - k/2 + 1 .. y + k/2 of the gradient feed pixel y
     (18, 36, 4, 10, "textured"),
     (15, 30, 6, 8, "quantized"),
     (1, 20, 2, 5, "textured"),
+    (24, 90, 16, 30, "smooth"),
+    (22, 120, 8, 64, "textured"),  # even k with D = 64 n: the last diagonal as a fifth chunk of sweeps
+    (30, 200, 10, 70, "textured"),
+    # generic fp64 backward (no fused instantiation): k > 17
+    (20, 44, 19, 9, "textured"),
+    (16, 40, 25, 12, "smooth"),
+    (17, 40, 18, 10, "textured"),
 ]
 
 
@@ -253,7 +265,7 @@ def test_backward_both_images(gpu, case, layout):
     assert np.abs(gp - rp).max() <= tol_p, np.abs(gp - rp).max() / max(1.0, np.abs(rp).max())
 
 
-@pytest.mark.parametrize("case", [(20, 44, 19, 9, "textured"), (18, 36, 4, 10, "smooth")], ids=["k19", "k4"])
+@pytest.mark.parametrize("case", [(20, 44, 19, 9, "textured"), (18, 40, 18, 10, "smooth")], ids=["k19", "k18"])
 @pytest.mark.parametrize("layout", [FULL, WIN])
 def test_backward_generic_small_bands(gpu, case, layout, monkeypatch):
     """The generic fp64 backward's band loop (A / VA / BA recomputed per band of output rows, halo
