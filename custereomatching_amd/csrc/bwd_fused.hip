@@ -236,7 +236,8 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     constexpr int FBC = fbc_for<K>();
     static_assert(FBC % (BDP + 1) == 0 && FBC <= 16, "flush blocks start on load buffer 0; 4 FBC lanes");
     constexpr int HPW = (NH + NWC - 1) / NWC;                // halo rows per wave (at most)
-    static_assert(HPW <= 4, "a wave's halo rows fit one quad of a 16-lane row");
+    static_assert(HPW <= 8, "a wave's halo rows fit one octet of a 16-lane row");
+    constexpr int HSL = HPW > 4 ? 8 : 4;  // halo camera slots per 16-lane row (lane l: halo row l % HSL)
 
     const ChunkGeo cg = chunk_geo(g, a.dlo, j);
     const int lane = threadIdx.x & 63;
@@ -376,11 +377,12 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     // stay inside the prepared array: rows checked per lane, columns per step)
     const i32x4 dPc = make_rsrc_sgpr(a.Xc, kWinNR);
     const int orow_l = y0i + yw + (lane & 3);  // own image row of this lane's quad slot
-    int hrow_l = -1;                           // halo image row of this lane's quad slot (or none)
-    if ((lane & 3) < HPW && wv + NWC * (lane & 3) < NH) hrow_l = (int)ir0 + halo_row(wv + NWC * (lane & 3));
+    int hrow_l = -1;                           // halo image row of this lane's halo slot (or none)
+    const int hq = lane & (HSL - 1);
+    if (hq < HPW && wv + NWC * hq < NH) hrow_l = (int)ir0 + halo_row(wv + NWC * hq);
     struct Ld {
         // xo / mc / cx: lane l holds own row l & 3 (row-replicated per 16 lanes, read back with
-        // DPP row_newbcast); xh: lane l holds the wave's halo row l & 3
+        // DPP row_newbcast); xh: lane l holds the wave's halo row l % HSL
         uint32_t ge[TRW], cv[TRW], hg[HP], xo, xh, mc, cx;
     };
     // NOP: open each load group with `s_nop 4` (VALU SGPR write -> VMEM read); the in-loop

@@ -135,6 +135,13 @@ size_t bwd_bytes(const Geo& g) {
     return fast_supported(g.k) ? backward_workspace_bytes(g) : backward_generic_workspace_bytes(g);
 }
 
+// The fast volume (precision FAST) keeps the north-star contract, |cost - reference| <= 1e-5, only
+// while the reference's own fp32 rounding stays below it in practice: measured for every k <= 17 in
+// the test matrix, while at k = 25 the fp64-exact sliding sums already differ from the reference's
+// k^2-long fp32 chain by 1.06e-5 (its worst-case bound (k^2 + 6) 2^-24 is 3.8e-5).  Larger k write
+// the exact volume (bit-identical); their fused disparity (certified) and backward still sweep.
+constexpr int kFastVolumeMaxK = 17;
+
 bool fast_supported(int k) {
     switch (k) {
 #define CUSTMA_K(KK) case KK:
@@ -223,7 +230,7 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     if (workspace_bytes < stats_bytes(g)) return fail(CUSTMA_E_WORKSPACE, "workspace too small");
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
-    const bool fast = precision == CUSTMA_FAST && fast_supported(g.k);
+    const bool fast = precision == CUSTMA_FAST && fast_supported(g.k) && g.k <= kFastVolumeMaxK;
     // the fast sweeps read sq and box only; the exact forward reads mean and sq
     // only the volume rows' statistics (a row band's halo rows feed the patches, not the statistics
     // the sweeps read)

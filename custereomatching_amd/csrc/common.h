@@ -195,6 +195,18 @@ __device__ __forceinline__ void asm_ld4s(uint32_t& a0, uint32_t& a1, uint32_t& a
 // Image-row groups for the forward sweep: 8 image loads (projector enter/leave x 2 halves,
 // camera enter/leave x 2 halves) / 6 statistics loads, rows selected by SGPR soffsets.
 // `s_nop 4` first: the soffsets may have been written by a VALU op (hazard note above).
+// Third camera register of the sweeps for 32 < 16 + k - 1 <= 48 columns (k = 19 .. 33): the entering and
+// leaving rows' columns 32 + (lane & 15) of the tile.
+template <typename T>
+__device__ __forceinline__ void asm_ld_img2(uint32_t& ce2, uint32_t& cl2, uint32_t vC2, i32x4 dC, uint32_t sE,
+                                            uint32_t sL) {
+    if constexpr (sizeof(T) == 4)
+        asm volatile("s_nop 4\n\tbuffer_load_dword %0, %2, %3, %4 offen\n\tbuffer_load_dword %1, %2, %3, %5 offen"
+                     : "=&v"(ce2), "=&v"(cl2) : "v"(vC2), "s"(dC), "s"(sE), "s"(sL));
+    else
+        asm volatile("s_nop 4\n\tbuffer_load_ushort %0, %2, %3, %4 offen\n\tbuffer_load_ushort %1, %2, %3, %5 offen"
+                     : "=&v"(ce2), "=&v"(cl2) : "v"(vC2), "s"(dC), "s"(sE), "s"(sL));
+}
 template <typename T>
 __device__ __forceinline__ void asm_ld_img8(uint32_t& pe0, uint32_t& pe1, uint32_t& pl0, uint32_t& pl1,
                                             uint32_t& ce0, uint32_t& ce1, uint32_t& cl0, uint32_t& cl1,

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     // taps rows h - R0 .. h + R1, columns w - R0 .. w + R1 (R0 = K/2, R1 = K-1-K/2: the reference's
     // kernel_size / 2 origin, stereo_matching_kernel.cu:44,60)
     constexpr int R0 = K / 2, R1 = K - 1 - K / 2, NX = TWT + K - 1;
-    static_assert(TWT == 16 && NX <= 32, "row-broadcast layout assumes 16 own columns and <= 32 taps");
+    static_assert(TWT == 16 && NX <= 48, "row-broadcast layout assumes 16 own columns and <= 48 camera columns");
     constexpr int NL_MAX = 320, LO = (NX + NL_MAX - 1 + 63) / 64, LS = (TWT + NL_MAX - 1 + 63) / 64;
     const int NL = sg.NL, NO = NX + NL - 1, NS = TWT + NL - 1;
     // LDS rows are padded to whole loader-lane chunks (OP = 64 LO, SP = 64 LS), so the loader
@@ -61,8 +61,8 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     constexpr int OP = 64 * LO, SP = 64 * LS;
     extern __shared__ __attribute__((aligned(16))) double ldsd[];
     double* ringO = ldsd;                  // [2 buf][2 enter/leave][OP] projector rows
-    double* ringU = ringO + 4 * OP;        // [2 buf][64]: +c of the entering row, -c of the leaving row
-    double* rsM = ringU + 2 * 64;          // [2][SP]  projector fp64 patch means
+    double* ringU = ringO + 4 * OP;        // [2 buf][2][64]: +c of the entering row, -c of the leaving row
+    double* rsM = ringU + 4 * 64;          // [2][SP]  projector fp64 patch means
     double* usB = rsM + 2 * SP;            // [2][64]  -(camera fp64 patch sums) (lanes 0-15)
     float* rsQ = (float*)(usB + 2 * 64);   // [2][SP]  projector ey2
     float* usQ = rsQ + 2 * SP;             // [2][64]  camera ex2 (lanes 0-15)
@@ -103,8 +103,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             return make_rsrc_sgpr((const char*)base + (ok ? row : 0) * g.W * esz, ok ? (uint32_t)(g.W * esz) : 0u);
         };
         uint32_t vO[LO], vSd[LS], vSf[LS];
-        const uint32_t vUe = colOff(li < NX, xU0 + li, sizeof(T));
-        const uint32_t vUl = colOff(li >= 32 && li - 32 < NX, xU0 + li - 32, sizeof(T));
+        const uint32_t vUe = colOff(li < NX, xU0 + li, sizeof(T));  // the leaving row: the same columns
         const uint32_t vUSd = colOff(li < TWT, u0 + li, 8), vUSf = colOff(li < TWT, u0 + li, 4);
 #pragma unroll
         for (int j = 0; j < LO; ++j) vO[j] = colOff(li + 64 * j < NO, xO0 + li + 64 * j, sizeof(T));
@@ -128,7 +127,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             const auto rCe = row_rsrc(cam, t + R1, sizeof(T), true), rCl = row_rsrc(cam, t - R0 - 1, sizeof(T), rem);
             const auto rPe = row_rsrc(proj, t + R1, sizeof(T), true), rPl = row_rsrc(proj, t - R0 - 1, sizeof(T), rem);
             asm_ld_raw<T>(p.ue, vUe, rCe);
-            asm_ld_raw<T>(p.ul, vUl, rCl);
+            asm_ld_raw<T>(p.ul, vUe, rCl);
 #pragma unroll
             for (int j = 0; j < LO; ++j) {
                 asm_ld_raw<T>(p.oe[j], vO[j], rPe);
@@ -159,7 +158,8 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             for (int j = 0; j < LS; ++j) { asm_tie(p.m[j]); asm_tie(p.q[j]); }
         };
         auto store_step = [&](int b, const Stage& p) {
-            ringU[b * 64 + li] = li < 32 ? raw_to_f64<T>(p.ue) : -raw_to_f64<T>(p.ul);  // 0 past NX
+            ringU[(2 * b) * 64 + li] = raw_to_f64<T>(p.ue);  // 0 past NX
+            ringU[(2 * b + 1) * 64 + li] = -raw_to_f64<T>(p.ul);
 #pragma unroll
             for (int j = 0; j < LO; ++j) {
                 ringO[(2 * b) * OP + li + 64 * j] = raw_to_f64<T>(p.oe[j]);
@@ -230,8 +230,10 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     const int r16 = tid & 15;
     // col[x] += c(enter, x) p(enter, x + delta) - c(leave, x) p(leave, x + delta)
     auto update = [&](int b) {
-        const double ca0 = ringU[b * 64 + r16], ca1 = ringU[b * 64 + 16 + r16];
-        const double cb0 = ringU[b * 64 + 32 + r16], cb1 = ringU[b * 64 + 48 + r16];  // negated
+        const double* ue = ringU + (2 * b) * 64;
+        const double* ul = ringU + (2 * b + 1) * 64;  // negated
+        const double ca0 = ue[r16], ca1 = ue[16 + r16], ca2 = NX > 32 ? ue[32 + r16] : 0.0;
+        const double cb0 = ul[r16], cb1 = ul[16 + r16], cb2 = NX > 32 ? ul[32 + r16] : 0.0;
         // volatile: keeps these as single ds_read_b64 (2 LDS cycles per wave-instruction)
         // instead of pairs merged into ds_read2_b64 (8 cycles, half the bandwidth)
         const lds_vd* oa = (const lds_vd*)(ringO + (2 * b) * OP + tid);
@@ -256,8 +258,8 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             if constexpr (bb + 1 < NB) fetch(std::integral_constant<int, bb + 1>{});
             Unroll<0, nb>::run([&](auto ic) {
                 constexpr int i = decltype(ic)::value, x = x0 + i;
-                fmac_bc64<(x & 15)>(col[x], x < 16 ? ca0 : ca1, pa[bb & 1][i]);
-                fmac_bc64<(x & 15)>(col[x], x < 16 ? cb0 : cb1, pb[bb & 1][i]);
+                fmac_bc64<(x & 15)>(col[x], x < 16 ? ca0 : x < 32 ? ca1 : ca2, pa[bb & 1][i]);
+                fmac_bc64<(x & 15)>(col[x], x < 16 ? cb0 : x < 32 ? cb1 : cb2, pb[bb & 1][i]);
             });
         });
     };
@@ -422,7 +424,7 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
     constexpr int NX = TW + K - 1;
     constexpr int NL_MAX = 320, OP = 64 * ((NX + NL_MAX - 1 + 63) / 64), SP = 64 * ((TW + NL_MAX - 1 + 63) / 64);
     const int NL = sg.NL;
-    const size_t lds = sizeof(double) * (4 * OP + 2 * 64 + 2 * SP + 2 * 64) +
+    const size_t lds = sizeof(double) * (4 * OP + 4 * 64 + 2 * SP + 2 * 64) +
                        sizeof(float) * (2 * SP + 2 * 64 + (part ? TW * (NL + 16) : 2 * TW * NL));
     const int64_t blocks = sweep_blocks(sg);
     if (part) {

@@ -86,7 +86,8 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     constexpr int AMX = AMX_ < 0 ? -AMX_ : AMX_;
     constexpr bool SOFT = AMX_ < 0;
     constexpr int R0 = K / 2, R1 = K - 1 - K / 2, NX = TW + K - 1;
-    static_assert(NX + 63 <= kRowP && NX <= 32, "row segment fits the LDS slice and two broadcast registers");
+    static_assert(NX + 63 <= kRowP && NX <= 48, "row segment fits the LDS slice and three broadcast registers");
+    constexpr bool C3R = NX > 32;  // a third camera register (columns 32 .. 47 of the tile, k >= 19)
     constexpr uint32_t OOB = 0x80000000u;
     // SS (STAGED): dword stores per thread per step, the same for every wave of the workgroup;
     // SS < 0: -SS 16-byte stores + one dword store (the block's < 4-float tail) per thread
@@ -103,6 +104,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     const int64_t xO0 = u0 - R0 + d0, oS = u0 + d0;
     const uint32_t vP0 = colOff(true, xO0 + l, sizeof(T)), vP1 = colOff(64 + l < NX + 64, xO0 + 64 + l, sizeof(T));
     const uint32_t vC0 = colOff(true, u0 - R0 + r16, sizeof(T)), vC1 = colOff(16 + r16 < NX, u0 - R0 + 16 + r16, sizeof(T));
+    const uint32_t vC2 = colOff(32 + r16 < NX, u0 - R0 + 32 + r16, sizeof(T));
     const uint32_t vM0 = colOff(true, oS + l, 8), vM1 = colOff(64 + l < TW + 64, oS + 64 + l, 8);
     const uint32_t vQ0 = colOff(true, oS + l, 4), vQ1 = colOff(64 + l < TW + 64, oS + 64 + l, 4);
     const uint32_t vUB = colOff(true, u0 + r16, 8), vUQ = colOff(true, u0 + r16, 4);
@@ -129,10 +131,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     };
 
     struct Stage {
-        uint32_t pe0, pe1, pl0, pl1, ce0, ce1, cl0, cl1, q0, q1, uq;
+        uint32_t pe0, pe1, pl0, pl1, ce0, ce1, cl0, cl1, ce2, cl2, q0, q1, uq;
         double m0, m1, ub;
     };
-    constexpr int kLoads = CPL ? 10 : 14;
+    constexpr int kLoads = CPL ? 10 : C3R ? 16 : 14;
     if constexpr (CPL) {
         // camera rows h0 - R0 + i (i < h1 - h0 + K - 1), columns u0 - R0 + j (j < NX), raw, 0 outside the image
         typedef __attribute__((address_space(3))) RawT lds_t;
@@ -152,8 +154,11 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         if constexpr (CPL)
             asm_ld_img4<T>(p.pe0, p.pe1, p.pl0, p.pl1, vP0, vP1, dProj, sE, sL);
         else
+        {
             asm_ld_img8<T>(p.pe0, p.pe1, p.pl0, p.pl1, p.ce0, p.ce1, p.cl0, p.cl1, vP0, vP1, vC0, vC1, dProj, dCam,
                            sE, sL);
+            if constexpr (C3R) asm_ld_img2<T>(p.ce2, p.cl2, vC2, dCam, sE, sL);
+        }
         const bool st = ti >= h0i && ti < h1i;
         asm_ld_stat6(p.m0, p.m1, p.q0, p.q1, p.ub, p.uq, vM0, vM1, vQ0, vQ1, vUB, vUQ, dPB, dPS, dCB, dCS,
                      so_row(ti, rb8, st), so_row(ti, rb4, st));
@@ -161,6 +166,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     auto tie = [&](Stage& p) {
         asm_tie(p.pe0); asm_tie(p.pe1); asm_tie(p.pl0); asm_tie(p.pl1);
         asm_tie(p.ce0); asm_tie(p.ce1); asm_tie(p.cl0); asm_tie(p.cl1);
+        if constexpr (C3R && !CPL) { asm_tie(p.ce2); asm_tie(p.cl2); }
         asm_tie(p.q0); asm_tie(p.q1); asm_tie(p.uq); asm_tie(p.m0); asm_tie(p.m1); asm_tie(p.ub);
     };
 
@@ -213,7 +219,11 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
         sM[64 + l] = p.m1 * rk2;
         sQ[l] = __builtin_bit_cast(float, p.q0);
         sQ[64 + l] = __builtin_bit_cast(float, p.q1);
-        uint32_t ce0 = p.ce0, ce1 = p.ce1, cl0 = p.cl0, cl1 = p.cl1;
+        uint32_t ce0 = p.ce0, ce1 = p.ce1, cl0 = p.cl0, cl1 = p.cl1, ce2 = 0u, cl2 = 0u;
+        if constexpr (C3R && !CPL) {
+            ce2 = p.ce2;
+            cl2 = p.cl2;
+        }
         if constexpr (CPL) {
             // the rows enter t + R1 and leave t - R0 - 1 (from t = h0 + 1 on) of the preloaded block
             typedef __attribute__((address_space(3))) const RawT lds_ct;
@@ -224,9 +234,15 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             ce1 = hi ? (uint32_t)cr[er * NX + 16 + r16] : 0u;
             cl0 = lv ? (uint32_t)cr[lr * NX + r16] : 0u;
             cl1 = lv && hi ? (uint32_t)cr[lr * NX + 16 + r16] : 0u;
+            if constexpr (C3R) {
+                const bool h2 = 32 + r16 < NX;
+                ce2 = h2 ? (uint32_t)cr[er * NX + 32 + r16] : 0u;
+                cl2 = lv && h2 ? (uint32_t)cr[lr * NX + 32 + r16] : 0u;
+            }
         }
         const double ca0 = raw_to_f64<T>(ce0), ca1 = raw_to_f64<T>(ce1);
         const double cb0 = -raw_to_f64<T>(cl0), cb1 = -raw_to_f64<T>(cl1);
+        const double ca2 = C3R ? raw_to_f64<T>(ce2) : 0.0, cb2 = C3R ? -raw_to_f64<T>(cl2) : 0.0;
         const double nb = -p.ub;                           // -(camera patch sum) of column r16
         const float uq = __builtin_bit_cast(float, p.uq);  // camera ex2 of column r16
 
@@ -250,26 +266,26 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 constexpr int bb = decltype(bc)::value, x0 = bb * B;
                 constexpr int nb_ = NX - x0 < B ? NX - x0 : B;
                 if constexpr (bb + 1 < NB) fetch(std::integral_constant<int, bb + 1>{});
-                const double a = x0 < 16 ? ca0 : ca1, b = x0 < 16 ? cb0 : cb1;  // x0 % 4 == 0
+                const double a = x0 < 16 ? ca0 : x0 < 32 ? ca1 : ca2, b = x0 < 16 ? cb0 : x0 < 32 ? cb1 : cb2;  // x0 % 4 == 0
                 const double* qa = pa[bb & 1];
                 const double* qb = pb[bb & 1];
                 if constexpr (nb_ == 4) {
-                    fmac2_bc64_x4<(x0 & 15), x0 == 0 || x0 == 16>(col[x0], col[x0 + 1], col[x0 + 2], col[x0 + 3], a, b, qa[0], qa[1],
+                    fmac2_bc64_x4<(x0 & 15), (x0 & 15) == 0>(col[x0], col[x0 + 1], col[x0 + 2], col[x0 + 3], a, b, qa[0], qa[1],
                                              qa[2], qa[3], qb[0], qb[1], qb[2], qb[3]);
                 } else if constexpr (nb_ == 2) {
-                    fmac2_bc64_x2<(x0 & 15), x0 == 0 || x0 == 16>(col[x0], col[x0 + 1], a, b, qa[0], qa[1], qb[0], qb[1]);
+                    fmac2_bc64_x2<(x0 & 15), (x0 & 15) == 0>(col[x0], col[x0 + 1], a, b, qa[0], qa[1], qb[0], qb[1]);
                 } else {
                     Unroll<0, nb_>::run([&](auto ic) {
                         constexpr int i = decltype(ic)::value, x = x0 + i;
-                        fmac_bc64<(x & 15), x0 == 0 || x0 == 16>(col[x], a, qa[i]);
-                        fmac_bc64<(x & 15), x0 == 0 || x0 == 16>(col[x], b, qb[i]);
+                        fmac_bc64<(x & 15), (x0 & 15) == 0>(col[x], a, qa[i]);
+                        fmac_bc64<(x & 15), (x0 & 15) == 0>(col[x], b, qb[i]);
                     });
                 }
             });
         }
 
         if constexpr (REM) {
-            const double cRe = l < 16 ? ca0 : ca1, cRl = l < 16 ? cb0 : cb1;  // camera column u0 - R0 + l
+            const double cRe = l < 16 ? ca0 : l < 32 ? ca1 : ca2, cRl = l < 16 ? cb0 : l < 32 ? cb1 : cb2;  // column u0 - R0 + l
             colR = __builtin_fma(cRe, *(const lds_vd*)(rowE + 64 + l), colR);
             colR = __builtin_fma(cRl, *(const lds_vd*)(rowL + 64 + l), colR);
         }

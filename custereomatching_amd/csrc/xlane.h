@@ -193,6 +193,29 @@ __device__ __forceinline__ void slide_rows<4>(uint32_t (&v)[12], uint32_t (&b)[1
         : "s"(lane63)
         : "vcc");
 }
+// More than 4 halo rows per wave (k >= 19): the first 4 as above, each further one by its own pair
+// (rotate the block register, lane 63 of the column from it).  hazard_check.py checks the listing.
+template <int HP>
+__device__ __forceinline__ void slide_rows(uint32_t (&v)[12], uint32_t (&b)[12], uint32_t (&hv)[HP], uint32_t (&hb)[HP],
+                                           uint64_t lane63) {
+    static_assert(HP > 4 && HP <= 8, "slide_rows: 1 .. 8 halo rows");
+    uint32_t v4[4] = {hv[0], hv[1], hv[2], hv[3]}, b4[4] = {hb[0], hb[1], hb[2], hb[3]};
+    slide_rows<4>(v, b, v4, b4, lane63);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        hv[i] = v4[i];
+        hb[i] = b4[i];
+    }
+#pragma unroll
+    for (int i = 4; i < HP; ++i)
+        asm volatile(
+            "s_mov_b64 vcc, %2\n\t"
+            "v_mov_b32_dpp %1, %1 wave_rol:1 row_mask:0xf bank_mask:0xf\n\t"
+            "v_cndmask_b32_dpp %0, %0, %1, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+            : "+v"(hv[i]), "+v"(hb[i])
+            : "s"(lane63)
+            : "vcc");
+}
 __device__ __forceinline__ float shl1_add(float acc, float v) {  // lane l <- acc[l+1] + v[l]; lane 63 <- v
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, acc), 0x130, 0xf, 0xf,
                                                                  true)) + v;

@@ -19,6 +19,9 @@ CFGS = {
     "c3_win_k8": dict(H=2048, W=2048, k=8, D=256, layout="window", dtype=torch.float16),
     "c3_win_k12": dict(H=2048, W=2048, k=12, D=256, layout="window", dtype=torch.float16),
     "c2_full_k10": dict(H=1024, W=1024, k=10, D=128, layout="full", dtype=torch.float32),
+    "c3_win_k19": dict(H=2048, W=2048, k=19, D=256, layout="window", dtype=torch.float16),
+    "c3_win_k25": dict(H=2048, W=2048, k=25, D=256, layout="window", dtype=torch.float16),
+    "c3_win_k31": dict(H=2048, W=2048, k=31, D=256, layout="window", dtype=torch.float16),
     # other sweep kernel sizes at C3 size
     "c3_win_k5": dict(H=2048, W=2048, k=5, D=256, layout="window", dtype=torch.float16),
     "c3_win_k9": dict(H=2048, W=2048, k=9, D=256, layout="window", dtype=torch.float16),

@@ -47,14 +47,18 @@ CASES = [
     (30, 64, 15, 31, "quantized"),
     (24, 48, 7, 0, "textured"),
     (26, 40, 5, 39, "textured"),
-    (19, 37, 21, 9, "textured"),  # beyond the sweep instantiations: exact kernel only
+    # odd k > 17: the volume is the exact kernel's (the fast volume stops at k = 17, capi.hip
+    # kFastVolumeMaxK); the sliding instantiations up to k = 31 serve the disparity and backward
+    (19, 37, 21, 9, "textured"),
+    (22, 60, 31, 12, "textured"),
+    (16, 40, 25, 9, "smooth"),
     (30, 70, 17, 31, "textured"),  # the largest sweep instantiation (16 + 2r = 32 columns)
     (20, 44, 4, 9, "textured"),   # even k: taps at -k/2 .. k/2-1 (reference .cu:44,60), sliding kernels
     (17, 33, 10, 6, "smooth"),
     (21, 50, 2, 11, "textured"),
     (26, 70, 16, 24, "quantized"),  # the largest even sliding instantiation (16 + 15 = 31 columns)
     (19, 45, 18, 9, "textured"),   # even k beyond the sliding instantiations: exact kernel only
-    (12, 70, 33, 20, "textured"),  # above the old limit of 31
+    (12, 70, 33, 20, "textured"),  # beyond the sliding instantiations: exact kernel only
     (24, 48, 5, 16, "constant"),
     (24, 48, 5, 16, "zeros"),
 ]
@@ -163,7 +167,8 @@ DISP_CASES = [
     (30, 64, 11, 16, "smooth"),
     (24, 48, 5, 16, "constant"),
     (24, 48, 5, 16, "zeros"),
-    (20, 40, 19, 12, "textured"),  # no sweep instance: every pixel decided exactly
+    (20, 40, 19, 12, "textured"),  # odd k > 17 on the sliding kernels
+    (20, 40, 33, 12, "textured"),  # no sweep instance: every pixel decided exactly
     (24, 64, 17, 20, "textured"),  # the largest sweep instance
     (20, 40, 4, 12, "textured"),   # even k (sliding kernels)
     (22, 70, 16, 20, "quantized"),
@@ -230,7 +235,7 @@ BWD_CASES = [
     (20, 100, 5, 64, "textured"),
     (18, 300, 11, 256, "smooth"),
     (16, 140, 15, 128, "quantized"),
-    # k = 17: the largest fused instantiation (one workgroup per CU: 92 KB of LDS)
+    # k = 17: one workgroup per CU (92 KB of LDS)
     (26, 80, 17, 20, "textured"),
     (20, 140, 17, 64, "smooth"),
     # even k on the fused sweep: rows / columns y - k/2 + 1 .. y + k/2 of the gradient feed pixel y
@@ -240,10 +245,14 @@ BWD_CASES = [
     (24, 90, 16, 30, "smooth"),
     (22, 120, 8, 64, "textured"),  # even k with D = 64 n: the last diagonal as a fifth chunk of sweeps
     (30, 200, 10, 70, "textured"),
-    # generic fp64 backward (no fused instantiation): k > 17
+    # odd k > 17 on the fused sweep (up to 8 halo rows per wave, one workgroup per CU)
     (20, 44, 19, 9, "textured"),
     (16, 40, 25, 12, "smooth"),
+    (20, 80, 31, 20, "textured"),
+    (18, 100, 21, 64, "quantized"),  # with D = 64 n: the remainder kernel at k = 21
+    # generic fp64 backward (no fused instantiation): even k > 16, k > 31
     (17, 40, 18, 10, "textured"),
+    (16, 44, 33, 10, "smooth"),
 ]
 
 
@@ -265,7 +274,7 @@ def test_backward_both_images(gpu, case, layout):
     assert np.abs(gp - rp).max() <= tol_p, np.abs(gp - rp).max() / max(1.0, np.abs(rp).max())
 
 
-@pytest.mark.parametrize("case", [(20, 44, 19, 9, "textured"), (18, 40, 18, 10, "smooth")], ids=["k19", "k18"])
+@pytest.mark.parametrize("case", [(20, 44, 33, 9, "textured"), (18, 40, 18, 10, "smooth")], ids=["k33", "k18"])
 @pytest.mark.parametrize("layout", [FULL, WIN])
 def test_backward_generic_small_bands(gpu, case, layout, monkeypatch):
     """The generic fp64 backward's band loop (A / VA / BA recomputed per band of output rows, halo
