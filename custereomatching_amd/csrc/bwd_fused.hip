@@ -391,6 +391,13 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     // WIN per-lane loop constants: the lane's diagonal (or the marker past D) and its camera-value
     // offsets (own row / halo row of its quad slot, each prepared array; the marker outside the image)
     const uint32_t vLane = dl <= g.D ? (uint32_t)dl * 4u : kWinNR;
+    // WIN: the rows' parts of the gradient / volume offsets folded into per-lane loop constants, so a
+    // step's loads all take the step's column as their one SGPR soffset (no per-load SALU add)
+    uint32_t vLO[TRW], vLH[HP];
+#pragma unroll
+    for (int m = 0; m < TRW; ++m) vLO[m] = vLane + sVo[m];
+#pragma unroll
+    for (int i = 0; i < HP; ++i) vLH[i] = vLane + sVh[i];
     auto img_row_a = [&](int row, int arr) -> uint32_t {
         return (row >= 0 && row < Hi) ? (uint32_t)(row * Wi * 4) + arr * pb4 : kWinNR;
     };
@@ -403,13 +410,15 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         if constexpr (WIN) {
             // wave-uniform parts: the step's volume column (marker outside [0, WO)) and the two
             // camera columns w and w - R (marker outside [0, W))
-            const uint32_t sW = (w >= 0 && w < (int)g.WO) ? (uint32_t)w * gsU4 : kWinNR;
+            // (w is wave-uniform; pinned to an SGPR so that sW, the loads' only soffset, is SALU-computed)
+            const int ws = __builtin_amdgcn_readfirstlane(w);
+            const uint32_t sW = (ws >= 0 && ws < (int)g.WO) ? (uint32_t)ws * gsU4 : kWinNR;
             const uint32_t sC = (w >= 0 && w < Wi) ? (uint32_t)w * 4u : kWinNR;
             const uint32_t sX = (xb >= 0 && xb < Wi) ? (uint32_t)xb * 4u : kWinNR;
 #pragma unroll
-            for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], vLane, vLane, dG, dV, sVo[m] + sW, sVo[m] + sW);
+            for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], vLO[m], vLO[m], dG, dV, sW, sW);
 #pragma unroll
-            for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], vLane, dG, sVh[i] + sW);
+            for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], vLH[i], dG, sW);
             if constexpr (!CAML) asm_ld4s<NOP>(b.xo, b.xh, b.mc, b.cx, vXo, vXh, vMo, vCo, dPc, sC, sX);
             return;
         }
@@ -537,7 +546,7 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             cxh_r = __builtin_bit_cast(uint32_t, cl[(12 + (q < HP ? q : HP - 1)) * kCamP + cc]);
         }
         issue(w + BDP, nxt, std::false_type{});  // past the segment's end: harmless, drained before the wave ends
-        float* Acur = Abuf + ((w - w0) & 1) * (NY * 64);  // double-buffered: one barrier per step
+        float* Acur = Abuf + ((w - w0) & 1) * ((NY + 1) * 64);  // double-buffered: one barrier per step
         // this wave's ring slot of the step (V of its rows K steps ago): wave-private, so read
         // ahead of the barrier
         float rsv[TRW];
@@ -568,14 +577,15 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             P[1][m] = shl1_add(P[1][m], Ae * rbc<m>(mco));
             P[2][m] = shl1_add(P[2][m], (V * af) * Xf);
         });
+        // halo rows: no per-step branch -- a wave without a last halo row computes it from its
+        // out-of-range (zero) loads anyway and stores it to the spare row NY of the A buffer
         Unroll<0, HPW>::run([&](auto ii) {
             constexpr int i = decltype(ii)::value;
+            constexpr bool ALL = NWC * i + NWC - 1 < NH;  // every wave has halo row i
             const int q = wv + NWC * i;
-            if (q < NH) {
-                const int y = halo_row(q);
-                Acur[y * 64 + lane] = F(cur.hg[i]) * __builtin_amdgcn_rsqf(
-                                                         __builtin_fmaf(rbc<i>(F(cxh_r)), F(shY[i]), kEps));
-            }
+            const int y = ALL || q < NH ? halo_row(q) : NY;
+            Acur[y * 64 + lane] = F(cur.hg[i]) * __builtin_amdgcn_rsqf(
+                                                     __builtin_fmaf(rbc<i>(F(cxh_r)), F(shY[i]), kEps));
         });
         if (s > 0) reduce_to(s - 1);
         __syncthreads();  // the unit's A rows of this step are published
@@ -842,7 +852,7 @@ __global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
     }
     if (sg >= chunk_nseg(chunk_geo(g, a.dlo, j), taps_of(g))) return;
     constexpr int NY = TRB + K - 1;
-    __shared__ __attribute__((aligned(16))) float Abuf[2 * NY * 64];
+    __shared__ __attribute__((aligned(16))) float Abuf[2 * (NY + 1) * 64];  // + a spare row (halo A of no row)
     __shared__ __attribute__((aligned(16))) float ring[NWC * K * TRW * 64];
     constexpr int FBC = fbc_for<K>();
     __shared__ __attribute__((aligned(16))) float cbuf[NWC][FBC][12];
@@ -1286,6 +1296,8 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     }
     // (gather and combine fused into one tiled pass -- the slot sums recomputed for each tile's r
     // halo -- measured slower: C5 backward op 29.5 -> 31.1 ms, C2 full 3.82 -> 3.95 ms)
+    // (a column-wise form, cover lists staged in LDS once per 64 columns and each slot read for 4-8 rows at
+    // once, measured slower: C5 1.82 -> 2.52-2.74 ms at 122-134 VGPRs against this kernel's 30)
     hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2), dim3(256), 0, s, g, a, acc,
                        a.remT, a.remT1);
     {

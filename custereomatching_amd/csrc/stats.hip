@@ -43,6 +43,7 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
                                                Stats st0, Stats st1, float* __restrict__ prep,
                                                const float* __restrict__ shift, int64_t ybeg, int64_t yend) {
     constexpr bool BOX_ONLY = MODE == STATS_BOX || MODE == STATS_BWD_PREP;
+    constexpr bool SQT = MODE != STATS_FWD;  // the fp64 sums of squares only feed sqt
     // blockIdx.z: 0 = camera, 1 = projector (one launch for both images)
     const T* __restrict__ img = blockIdx.z ? img1 : img0;
     const Stats st = blockIdx.z ? st1 : st0;
@@ -66,10 +67,10 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
         for (int j = 0; j < k; ++j) {
             const double v = (double)t[j];
             a += v;
-            b = fma(v, v, b);
+            if constexpr (SQT) b = fma(v, v, b);
         }
         rs[e] = a;
-        rs2[e] = b;
+        if constexpr (SQT) rs2[e] = b;
     }
     __syncthreads();
     const int lx = threadIdx.x % TX, q = threadIdx.x / TX;  // rows PR q .. PR q + PR-1
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
 #pragma unroll
         for (int i = 0; i < k; ++i) {
             b += rs[(ly + i) * TX + lx];
-            b2 += rs2[(ly + i) * TX + lx];
+            if constexpr (SQT) b2 += rs2[(ly + i) * TX + lx];
         }
         const int64_t o = y * g.W + x;
         if constexpr (MODE == STATS_FULL) st.mean[o] = m[p];

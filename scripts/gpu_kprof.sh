@@ -1,20 +1,21 @@
 #!/bin/bash
-# Per-kernel durations (rocprofv3 kernel trace) of kbench ops, per library variant, one box.
-# Usage: bash scripts/gpu_kprof.sh <tag> <cfgs> <ops> "<name>:<variant|base>:<ENV=V,...>" ...
+# Backward-subset GPU tests, then a rocprofv3 kernel-trace summary of kbench ops.
+# Usage: bash scripts/gpu_kprof.sh <tag> <cfgs> <ops> [pytest -k expr]
 set -o pipefail
-TAG=$1; CFG=$2; OPS=$3; shift 3
+TAG=$1; CFGS=$2; OPS=$3; TK=${4:-backward}
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-for spec in "$@"; do
-  IFS=: read -r NAME V ENVS <<< "$spec"
-  L=$PWD/scripts/_abl/$V/libcustma_hip.so
-  [ "$V" = "base" ] && L=$PWD/custereomatching_amd/_lib/libcustma_hip.so
-  EV=$(echo "$ENVS" | tr ',' ' ')
-  for c in ${CFG//,/ }; do
-    env CUSTMA_LIB=$L $EV timeout -k 10 300 rocprofv3 --kernel-trace -d $O/${NAME}_$c -o run --output-format csv -- python3 scripts/kbench.py --cfg $c --ops $OPS --reps 4 > $O/${NAME}_$c.log 2>&1 || { echo "$NAME $c failed"; tail -5 $O/${NAME}_$c.log; exit 1; }
-    f=$(find $O/${NAME}_$c -name "*kernel_trace.csv" | head -1)
-    python3 scripts/ktrace_summary.py "$f" "$NAME $c"
-  done
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$TK" > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 scripts/kbench.py --cfg $CFGS --ops $OPS --reps 5 > $O/kbench.log 2>&1 || { echo "rocprof failed"; tail -20 $O/kbench.log; exit 1; }
+grep cfg $O/kbench.log
+f=$(find $O/prof -name "*kernel_stats.csv" | head -1)
+cp "$f" $O/kernel_stats.csv
+python3 - "$f" <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    n = r["Name"]; i = n.find("k_"); n = n[i:i + 70] if i >= 0 else n[:70]
+    print(f"{float(r['AverageNs'])/1e3:10.1f} us x{r['Calls']:>4}  {n}")
+PY
