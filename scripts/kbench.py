@@ -11,6 +11,7 @@ CFGS = {
     "c2_win": dict(H=1024, W=1024, k=9, D=128, layout="window", dtype=torch.float32),
     "c3_win": dict(H=2048, W=2048, k=11, D=256, layout="window", dtype=torch.float16),
     "c3_full": dict(H=2048, W=2048, k=11, D=256, layout="full", dtype=torch.float16),
+    "c3_win_d255": dict(H=2048, W=2048, k=11, D=255, layout="window", dtype=torch.float16),
     "c5_win": dict(H=4096, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
     # kernel sizes without a sweep instantiation (exact forward + generic fp64 backward)
     "c3_win_k17": dict(H=2048, W=2048, k=17, D=256, layout="window", dtype=torch.float16),
@@ -50,9 +51,11 @@ def run(name, ops, reps):
             for _ in range(reps):
                 et.record(lambda: cm.cost_volume_forward(cam, proj, D, k, lay, prec, out=out))
             ms = et.mean_ms()
-            kms, _ = _lib.profile_mean_ms(_lib.PROF_FWD)
+            kms, nk = _lib.profile_mean_ms(_lib.PROF_FWD)
             _lib.profile_enable(False)
-            res[f"fwd_{prec}_kernel_ms"] = round(kms, 4)
+            res[f"fwd_{prec}_kernel_ms"] = round(kms, 4)  # per sweep launch
+            if nk != reps:
+                res[f"fwd_{prec}_launches_per_op"] = round(nk / reps, 2)
             nb = out.numel() * 4 + 2 * H * W * cam.element_size()
             res[f"fwd_{prec}_ms"] = round(ms, 4)
             res[f"fwd_{prec}_GBps"] = round(nb / ms / 1e6, 1)
