@@ -234,7 +234,7 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     // the fast sweeps read sq and box only; the exact forward reads mean and sq
     // only the volume rows' statistics (a row band's halo rows feed the patches, not the statistics
     // the sweeps read)
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, fast ? STATS_FWD : STATS_FULL,
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, fast ? STATS_FWD : STATS_MSB,
                         STATS_BAND_ROWS)))
         return rc;
     if (fast)
@@ -339,7 +339,7 @@ int custma_disparity_band(const void* camera, const void* projector, int32_t dty
         return fail(CUSTMA_E_WORKSPACE, "workspace too small");
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, STATS_FULL, STATS_BAND_ROWS))) return rc;
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, STATS_MSB, STATS_BAND_ROWS))) return rc;
     void* ws2 = (char*)workspace + stats_bytes(g);
     return check_hip(launch_disparity(camera, projector, dtype, g, sc, sp, index, best, n_rechecked, ws2, s, nullptr,
                                       0.f, nullptr, 0.f),
@@ -360,7 +360,7 @@ int custma_disparity_soft_band(const void* camera, const void* projector, int32_
         return fail(CUSTMA_E_WORKSPACE, "workspace too small");
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
-    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, STATS_FULL, STATS_BAND_ROWS))) return rc;
+    if ((rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, STATS_MSB, STATS_BAND_ROWS))) return rc;
     void* ws2 = (char*)workspace + stats_bytes(g);
     return check_hip(launch_disparity(camera, projector, dtype, g, sc, sp, index, best, n_rechecked, ws2, s, soft,
                                       beta, mask, threshold),

@@ -347,10 +347,11 @@ hipError_t launch_u8_to_unit(const uint8_t* src, int64_t npix, int C, int ch, in
                              hipStream_t s);
 // Which statistics launch_stats writes (stats.hip k_stats): FULL = mean, sq, box, sqt; BOX = box, sqt (the
 // generic backward); BWD_PREP = box + the fused backward's prepared images (`prep`, needs `shift`); FWD = sq,
-// box (what the fast forward sweeps read).  BAND: only the volume rows [h_lo, h_hi) (a forward or disparity
+// box (what the fast forward sweeps read); MSB = mean, sq, box (the disparity and the exact forward: no sums of
+// squares).  BAND: only the volume rows [h_lo, h_hi) (a forward or disparity
 // reads the statistics of its volume rows only: voxel (h, w, d) the camera's at (h, w), the projector's at
 // (h, d)); otherwise every image row (the backward reads its gradient rows and their halo).
-enum StatsMode { STATS_FULL = 0, STATS_BOX = 1, STATS_BWD_PREP = 2, STATS_FWD = 3 };
+enum StatsMode { STATS_FULL = 0, STATS_BOX = 1, STATS_BWD_PREP = 2, STATS_FWD = 3, STATS_MSB = 4 };
 enum StatsRows { STATS_ALL_ROWS = 0, STATS_BAND_ROWS = 1 };
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
                         int mode = STATS_FULL, float* prep = nullptr, const float* shift = nullptr,

@@ -38,12 +38,14 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 //   STATS_BWD_PREP  box and the fused sweep's prepared fp32 images (bwd_fused.hip k_bwd_sweep's
 //                   X = sqt, m' = box / k^2 - shift, raw image; image z at prep + 3 z planes)
 //   STATS_FWD       sq, box                   (what the fast forward sweeps read)
+//   STATS_MSB       mean, sq, box             (the disparity: its sweep reads sq, box, its exact
+//                                              recheck mean, sq; the exact forward reads mean, sq)
 template <typename T, int KT, int MODE>
 __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const T* __restrict__ img1, Geo g,
                                                Stats st0, Stats st1, float* __restrict__ prep,
                                                const float* __restrict__ shift, int64_t ybeg, int64_t yend) {
     constexpr bool BOX_ONLY = MODE == STATS_BOX || MODE == STATS_BWD_PREP;
-    constexpr bool SQT = MODE != STATS_FWD;  // the fp64 sums of squares only feed sqt
+    constexpr bool SQT = MODE != STATS_FWD && MODE != STATS_MSB;  // the fp64 sums of squares only feed sqt
     // blockIdx.z: 0 = camera, 1 = projector (one launch for both images)
     const T* __restrict__ img = blockIdx.z ? img1 : img0;
     const Stats st = blockIdx.z ? st1 : st0;
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(256) void k_stats(const T* __restrict__ img0, const
             if constexpr (SQT) b2 += rs2[(ly + i) * TX + lx];
         }
         const int64_t o = y * g.W + x;
-        if constexpr (MODE == STATS_FULL) st.mean[o] = m[p];
+        if constexpr (MODE == STATS_FULL || MODE == STATS_MSB) st.mean[o] = m[p];
         st.sq[o] = sq[p];
         st.box[o] = b;
         if constexpr (MODE == STATS_FULL) {
@@ -236,6 +238,7 @@ hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo&
                 case STATS_BOX: launch(cast, std::integral_constant<int, STATS_BOX>{}); break;
                 case STATS_BWD_PREP: launch(cast, std::integral_constant<int, STATS_BWD_PREP>{}); break;
                 case STATS_FWD: launch(cast, std::integral_constant<int, STATS_FWD>{}); break;
+                case STATS_MSB: launch(cast, std::integral_constant<int, STATS_MSB>{}); break;
                 default: launch(cast, std::integral_constant<int, STATS_FULL>{});
             }
         };
