@@ -1,8 +1,11 @@
 // C ABI of libcustma_hip.so (declared in include/custma.h).
-// Validation, workspace carving and dispatch; no allocation, no
-// synchronisation (graph-capturable).  Error behaviour: every entry point
-// returns a CUSTMA_E_* code and records a message for custma_last_error(),
-// which the Python shim raises as RuntimeError / ValueError -- unlike the
+// Validation, workspace carving and dispatch; no allocation, no host
+// synchronisation (graph-capturable).  The one piece of library state is a
+// per-device side stream with two events (created on first use), which an
+// eager large fast forward forks onto and joins back from (forward_split).
+// Error behaviour: every entry point returns a CUSTMA_E_* code and records a
+// message for custma_last_error(), which the Python shim raises as
+// RuntimeError / ValueError -- unlike the
 // reference, which checks only device/contiguity (custma/include/
 // stereo_matching.hpp:20-33), asserts the shape in debug builds only
 // (custma/src/stereo_matching.cpp:28) and never checks its launches
@@ -89,6 +92,47 @@ int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, vo
     return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s, mode, nullptr, nullptr, rows), "stats");
 }
 
+// The fast window forward of a large band as two halves, so that the second half's statistics pass
+// runs beside the first half's sweep instead of in front of the whole sweep:
+//   s:    stats(A) -> fork -> sweep(A) ........................ wait(join)
+//   side:                    wait(fork) -> stats(B) -> sweep(B) -> join
+// (the halves' statistics and volume rows are disjoint; a half keeps the whole band's row-band
+// height, so the two sweeps launch the same blocks the single sweep would).  Stream order on s is
+// kept: the side stream starts after everything enqueued on s before the call, and s continues
+// after both halves.
+bool split_forward(const Geo& g) {
+    if (g.layout != CUSTMA_LAYOUT_WINDOW || !disp_tile_ok(g)) return false;
+    const int th = wave_grid(g).TH;
+    return g.HV() >= 8 * th && (double)g.HV() * g.WO * g.DO * 4 >= 1e9;
+}
+
+int forward_split(const void* cam, const void* proj, int32_t dtype, const Geo& g, void* ws, float* out,
+                  hipStream_t s) {
+    SideStream sd;
+    std::unique_lock<std::mutex> lock;
+    int rc = check_hip(side_stream(&sd, &lock), "side stream");
+    if (rc) return rc;
+    SideStream* side = &sd;
+    Geo ga = g, gb = g;
+    ga.band_rows = gb.band_rows = wave_grid(g).TH;
+    const int64_t half = cdiv(cdiv(g.HV(), 2), ga.band_rows) * ga.band_rows;
+    ga.h_hi = gb.h_lo = g.h_lo + half;
+    Stats sc, sp;
+    carve_stats(g, ws, &sc, &sp);
+    if ((rc = check_hip(launch_stats(cam, proj, dtype, ga, sc, sp, s, STATS_FWD, nullptr, nullptr, STATS_BAND_ROWS),
+                        "stats")) ||
+        (rc = check_hip(hipEventRecord(side->fork, s), "fork")) ||
+        (rc = check_hip(launch_fwd_fast(cam, proj, dtype, ga, sc, sp, out, s), "forward(fast)")) ||
+        (rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "fork wait")) ||
+        (rc = check_hip(launch_stats(cam, proj, dtype, gb, sc, sp, side->s, STATS_FWD, nullptr, nullptr,
+                                     STATS_BAND_ROWS), "stats")) ||
+        (rc = check_hip(launch_fwd_fast(cam, proj, dtype, gb, sc, sp, out + half * g.WO * g.DO, side->s),
+                        "forward(fast)")) ||
+        (rc = check_hip(hipEventRecord(side->join, side->s), "join")))
+        return rc;
+    return check_hip(hipStreamWaitEvent(s, side->join, 0), "join wait");
+}
+
 int check_dtype(int32_t dtype) {
     if (dtype != CUSTMA_F32 && dtype != CUSTMA_F16)
         return fail(CUSTMA_E_ARG, "unsupported dtype code %d (float32=0, float16=1)", dtype);
@@ -141,6 +185,27 @@ size_t bwd_bytes(const Geo& g) {
 // k^2-long fp32 chain by 1.06e-5 (its worst-case bound (k^2 + 6) 2^-24 is 3.8e-5).  Larger k write
 // the exact volume (bit-identical); their fused disparity (certified) and backward still sweep.
 constexpr int kFastVolumeMaxK = 17;
+
+// Side stream of the current device (non-blocking, created once and kept for the process's lifetime,
+// like the runtime's own per-device state), with its fork / join events.
+hipError_t side_stream(SideStream* out, std::unique_lock<std::mutex>* lock) {
+    static std::mutex mu[64];
+    static SideStream ss[64];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    *lock = std::unique_lock<std::mutex>(mu[dev]);
+    SideStream& x = ss[dev];
+    if (!x.s) {
+        if ((e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&x.join, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking)) != hipSuccess)
+            return e;
+    }
+    *out = x;
+    return hipSuccess;
+}
 
 bool fast_supported(int k) {
     switch (k) {
@@ -231,6 +296,13 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
     const bool fast = precision == CUSTMA_FAST && fast_supported(g.k) && g.k <= kFastVolumeMaxK;
+    // (eager calls only: under stream capture the single-stream form is recorded)
+    if (fast && split_forward(g)) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone)
+            return forward_split(camera, projector, dtype, g, workspace, cost_volume, s);
+        (void)hipGetLastError();  // a refused query must not read as a later launch's failure
+    }
     // the fast sweeps read sq and box only; the exact forward reads mean and sq
     // only the volume rows' statistics (a row band's halo rows feed the patches, not the statistics
     // the sweeps read)

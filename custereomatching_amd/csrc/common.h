@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/custma.h"
 
 namespace custma {
@@ -22,6 +24,7 @@ struct Geo {
     int32_t D;
     int64_t WO, DO; // volume [h_hi - h_lo, WO, DO]
     int64_t h_lo, h_hi;  // volume rows = image rows [h_lo, h_hi) (row bands: the rest is halo)
+    int32_t band_rows = 0;  // fast forward sweeps' row-band height (0: wave_grid's choice)
     __host__ __device__ int64_t HV() const { return h_hi - h_lo; }
 };
 
@@ -347,10 +350,20 @@ hipError_t launch_u8_to_unit(const uint8_t* src, int64_t npix, int C, int ch, in
                              hipStream_t s);
 // Which statistics launch_stats writes (stats.hip k_stats): FULL = mean, sq, box, sqt; BOX = box, sqt (the
 // generic backward); BWD_PREP = box + the fused backward's prepared images (`prep`, needs `shift`); FWD = sq,
-// box (what the fast forward sweeps read); MSB = mean, sq, box (the disparity and the exact forward: no sums of
-// squares).  BAND: only the volume rows [h_lo, h_hi) (a forward or disparity
+// box (what the fast forward sweeps read).  BAND: only the volume rows [h_lo, h_hi) (a forward or disparity
 // reads the statistics of its volume rows only: voxel (h, w, d) the camera's at (h, w), the projector's at
 // (h, d)); otherwise every image row (the backward reads its gradient rows and their halo).
+// Per-device side stream with fork / join events (capi.hip): the launches that run beside the main
+// stream's work (the split forward, the backward's remainder-diagonal pass) fork onto it after an
+// event on the caller's stream and join back before anything that reads their results.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+// The current device's side stream; `lock` guards a fork ... join enqueue sequence (the events are
+// shared, and a wait binds to the most recent record at the time it is enqueued).
+hipError_t side_stream(SideStream* out, std::unique_lock<std::mutex>* lock);
+
 enum StatsMode { STATS_FULL = 0, STATS_BOX = 1, STATS_BWD_PREP = 2, STATS_FWD = 3, STATS_MSB = 4 };
 enum StatsRows { STATS_ALL_ROWS = 0, STATS_BAND_ROWS = 1 };
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,

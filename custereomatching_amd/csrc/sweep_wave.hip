@@ -644,6 +644,7 @@ WaveGrid wave_grid(const Geo& g) {
     wg.TH = 64;  // band height (32 / 128 measured within 2 %)
     // keep >= ~8 waves per SIMD on small problems
     while (wg.TH > 8 && (int64_t)wg.nTile * wg.nChunk * cdiv(g.HV(), wg.TH) < 8192) wg.TH /= 2;
+    if (g.band_rows > 0) wg.TH = g.band_rows;  // a part of a split forward keeps the whole band's height
     wg.nBand = (int)cdiv(g.HV(), wg.TH);
     return wg;
 }

@@ -543,3 +543,56 @@ def test_disparity_soft_argmax_and_mask(gpu, case, kind):
     w = np.arange(ref.shape[1], dtype=np.float32)
     want = ((-ridx if layout == "window" else w - ridx) * (rbest > thr)).astype(np.float32)
     assert np.array_equal(dmap.cpu().numpy(), want)
+
+
+# ---- the split forward (capi.hip forward_split): a >= 1 GB window volume is swept as two half-band
+# launches on two streams, the second half's statistics pass beside the first half's sweep ----
+
+def _split_inputs(gpu):
+    H, W, D, k = 1024, 1280, 256, 11  # [1024, 1024, 257] fp32 = 1.08 GB
+    cam, proj = make_pair(H, W, D, seed=61)
+    return _dev(cam, gpu, torch.float16), _dev(proj, gpu, torch.float16), H, D, k
+
+
+def test_split_forward_matches_half_bands(gpu):
+    """The two-stream forward equals the same rows computed as two separate band calls (each below the
+    split size), bit for bit, and stays within the fast tolerance of the exact volume."""
+    c, p, H, D, k = _split_inputs(gpu)
+    full = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
+    torch.cuda.synchronize()
+    r0, r1 = k // 2, k - 1 - k // 2
+    for b, e in ((0, 300), (300, 700), (700, H)):
+        a0, a1 = max(0, b - r0), min(H, e + r1)
+        vb = cm.cost_volume_forward(c[a0:a1].contiguous(), p[a0:a1].contiguous(), D, k, WIN, "fast",
+                                    rows=(b - a0, e - a0))
+        assert torch.equal(vb, full[b:e]), (b, e)
+        del vb
+    for h0 in (0, 509, 1016):
+        ex = cm.cost_volume_forward(c[max(0, h0 - r0):h0 + 8 + r1].contiguous(),
+                                    p[max(0, h0 - r0):h0 + 8 + r1].contiguous(), D, k, WIN, "exact",
+                                    rows=(h0 - max(0, h0 - r0), h0 - max(0, h0 - r0) + 8))
+        assert float((ex - full[h0:h0 + 8]).abs().max()) <= O.fast_tolerance(k)
+
+
+def test_split_forward_graph_capture(gpu):
+    """Under stream capture the forward records its single-stream form (capi.hip: the side-stream
+    split is for eager calls): a replay on new inputs equals the eager (split) forward bit for bit."""
+    c, p, H, D, k = _split_inputs(gpu)
+    out = torch.empty(H, c.shape[1] - D, D + 1, device=gpu)
+    side = torch.cuda.Stream(gpu)
+    side.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(side):
+        cm.cost_volume_forward(c, p, D, k, WIN, "fast", out=out)  # warm-up outside the capture
+    torch.cuda.current_stream(gpu).wait_stream(side)
+    torch.cuda.synchronize(gpu)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        cm.cost_volume_forward(c, p, D, k, WIN, "fast", out=out)
+    c2, p2 = make_pair(H, c.shape[1], D, seed=62)
+    with torch.no_grad():
+        c.copy_(_dev(c2, gpu, torch.float16))
+        p.copy_(_dev(p2, gpu, torch.float16))
+    graph.replay()
+    torch.cuda.synchronize(gpu)
+    ref = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
+    assert torch.equal(out, ref)
