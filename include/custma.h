@@ -11,10 +11,14 @@
  * contiguous, of element type `dtype`.  Outputs are written fully (no
  * pre-zeroing needed).  `workspace` is device memory of at least
  * custma_workspace_bytes(...) bytes, owned by the caller (the torch caching
- * allocator in the Python shim); nothing is allocated inside a call, no
- * internal stream or event is used and nothing synchronises, so every call is
- * hipGraph-capturable (tests/test_gpu_graph.py captures forward + backward
- * into a torch.cuda.CUDAGraph and replays it bit-identically).
+ * allocator in the Python shim); no device memory is allocated inside a call
+ * and nothing synchronises the host.  Work runs on `stream`, except that an
+ * eager (not capturing) fast window forward of >= 1 GB forks its second half
+ * onto a per-device side stream the library creates once, and makes `stream`
+ * wait for it before returning (stream order is unchanged).  Under capture
+ * every call stays on `stream`, so every call is hipGraph-capturable
+ * (tests/test_gpu_graph.py captures forward + backward into a
+ * torch.cuda.CUDAGraph and replays it bit-identically).
  */
 #ifndef CUSTMA_H
 #define CUSTMA_H
