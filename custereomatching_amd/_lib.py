@@ -23,7 +23,8 @@ E_ARG, E_NULL, E_WORKSPACE, E_LAUNCH, E_UNSUPPORTED = -1, -2, -3, -4, -5
 EXPORTS = ("custma_abi_version", "custma_last_error", "custma_volume_dims", "custma_workspace_bytes",
            "custma_forward", "custma_backward", "custma_argmax", "custma_disparity", "custma_forward_band",
            "custma_backward_band", "custma_disparity_band", "custma_profile_enable", "custma_profile_mean_ms",
-           "custma_image_u8_to_unit", "custma_disparity_soft_band")
+           "custma_image_u8_to_unit", "custma_disparity_soft_band", "custma_patch_stats")
+STATS_FULL, STATS_BOX, STATS_BWD_PREP, STATS_FWD, STATS_MSB = 0, 1, 2, 3, 4
 
 
 class CustmaError(RuntimeError):
@@ -56,11 +57,12 @@ def _load():
     lib.custma_disparity_soft_band.argtypes = [vp, vp, i32, i64, i64, i32, i32, i32, i64, i64, f32, f32, vp, vp, vp,
                                                vp, vp, vp, sz, vp]
     lib.custma_profile_enable.argtypes = [i32]
+    lib.custma_patch_stats.argtypes = [vp, vp, i32, i64, i64, i32, i32, i64, i64, vp, vp, vp, vp, vp, vp, vp]
     lib.custma_image_u8_to_unit.argtypes = [vp, i64, i64, i32, i32, i32, vp, vp]
     lib.custma_profile_mean_ms.argtypes = [i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int32)]
     for name in ("custma_profile_enable", "custma_profile_mean_ms", "custma_forward", "custma_backward", "custma_argmax", "custma_disparity",
                  "custma_volume_dims", "custma_forward_band", "custma_backward_band", "custma_disparity_band",
-                 "custma_image_u8_to_unit", "custma_disparity_soft_band"):
+                 "custma_image_u8_to_unit", "custma_disparity_soft_band", "custma_patch_stats"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
 

@@ -101,6 +101,9 @@ int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, vo
 // kept: the side stream starts after everything enqueued on s before the call, and s continues
 // after both halves.
 bool split_forward(const Geo& g) {
+    // CUSTMA_FWD_SPLIT=0 keeps the single-stream form (same-box A/B, scripts/kbench.py)
+    const char* e = getenv("CUSTMA_FWD_SPLIT");
+    if (e && e[0] == '0') return false;
     if (g.layout != CUSTMA_LAYOUT_WINDOW || !disp_tile_ok(g)) return false;
     const int th = wave_grid(g).TH;
     return g.HV() >= 8 * th && (double)g.HV() * g.WO * g.DO * 4 >= 1e9;
@@ -121,16 +124,33 @@ int forward_split(const void* cam, const void* proj, int32_t dtype, const Geo& g
     carve_stats(g, ws, &sc, &sp);
     if ((rc = check_hip(launch_stats(cam, proj, dtype, ga, sc, sp, s, STATS_FWD, nullptr, nullptr, STATS_BAND_ROWS),
                         "stats")) ||
-        (rc = check_hip(hipEventRecord(side->fork, s), "fork")) ||
-        (rc = check_hip(launch_fwd_fast(cam, proj, dtype, ga, sc, sp, out, s), "forward(fast)")) ||
-        (rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "fork wait")) ||
-        (rc = check_hip(launch_stats(cam, proj, dtype, gb, sc, sp, side->s, STATS_FWD, nullptr, nullptr,
-                                     STATS_BAND_ROWS), "stats")) ||
-        (rc = check_hip(launch_fwd_fast(cam, proj, dtype, gb, sc, sp, out + half * g.WO * g.DO, side->s),
-                        "forward(fast)")) ||
-        (rc = check_hip(hipEventRecord(side->join, side->s), "join")))
+        (rc = check_hip(hipEventRecord(side->fork, s), "fork")))
         return rc;
-    return check_hip(hipStreamWaitEvent(s, side->join, 0), "join wait");
+    // from the fork on, the side stream is joined back into s whatever fails below: nothing the
+    // side stream may still write (statistics, volume rows) outlives the caller's stream order
+    if (!(rc = check_hip(launch_fwd_fast(cam, proj, dtype, ga, sc, sp, out, s), "forward(fast)")) &&
+        !(rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "fork wait")) &&
+        !(rc = check_hip(launch_stats(cam, proj, dtype, gb, sc, sp, side->s, STATS_FWD, nullptr, nullptr,
+                                      STATS_BAND_ROWS), "stats")))
+        rc = check_hip(launch_fwd_fast(cam, proj, dtype, gb, sc, sp, out + half * g.WO * g.DO, side->s),
+                       "forward(fast)");
+    const int rj = check_hip(hipEventRecord(side->join, side->s), "join");
+    const int rw = rj ? rj : check_hip(hipStreamWaitEvent(s, side->join, 0), "join wait");
+    return rc ? rc : rw;
+}
+
+// The side stream belongs to the current device; a caller's stream of another device keeps the
+// single-stream form.
+bool stream_on_current_device(hipStream_t s) {
+    int cur = 0;
+    hipDevice_t sd = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return false;
+    if (!s) return true;
+    if (hipStreamGetDevice(s, &sd) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return (int)sd == cur;
 }
 
 int check_dtype(int32_t dtype) {
@@ -297,7 +317,7 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     Stats sc, sp;
     const bool fast = precision == CUSTMA_FAST && fast_supported(g.k) && g.k <= kFastVolumeMaxK;
     // (eager calls only: under stream capture the single-stream form is recorded)
-    if (fast && split_forward(g)) {
+    if (fast && split_forward(g) && stream_on_current_device(s)) {
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone)
             return forward_split(camera, projector, dtype, g, workspace, cost_volume, s);
@@ -347,16 +367,20 @@ int custma_backward_band(const float* grad, const float* cost_volume, const void
     // Statistics: a recompute needs the forward's (sq, box for the fast sweep; mean, sq for the exact
     // one); given the forward's volume, the generic backward reads box and sqt, and the fused one
     // computes its own (box + prepared images, one pass inside launch_backward) -- the k^2-long fp32
-    // chains of mean / sq are skipped either way
-    if (!cost_volume) rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, fused ? STATS_FWD : STATS_FULL);
+    // chains of mean / sq are skipped either way.  The recomputed volume is the one the forward
+    // returns (custma_forward_band): the fast sweep only up to kFastVolumeMaxK, the exact kernel above.
+    const bool fast_vol = fused && g.k <= kFastVolumeMaxK;
+    if (!cost_volume)
+        rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s,
+                       fast_vol ? STATS_FWD : fused ? STATS_MSB : STATS_FULL);
     else if (!fused) rc = run_stats(camera, projector, dtype, g, workspace, &sc, &sp, s, STATS_BOX);
     else carve_stats(g, workspace, &sc, &sp);
     if (rc) return rc;
     char* ws2 = (char*)workspace + stats_bytes(g);
     if (!cost_volume) {  // recompute the forward into the workspace
         float* vol = (float*)(ws2 + align256(bwd_bytes(g)));
-        const hipError_t e = fused ? launch_fwd_fast(camera, projector, dtype, g, sc, sp, vol, s)
-                                   : launch_fwd_exact(camera, projector, dtype, g, sc, sp, vol, s);
+        const hipError_t e = fast_vol ? launch_fwd_fast(camera, projector, dtype, g, sc, sp, vol, s)
+                                      : launch_fwd_exact(camera, projector, dtype, g, sc, sp, vol, s);
         if ((rc = check_hip(e, "backward(recompute)"))) return rc;
         cost_volume = vol;
     }
@@ -367,6 +391,23 @@ int custma_backward_band(const float* grad, const float* cost_volume, const void
     return check_hip(launch_backward(grad, cost_volume, camera, projector, dtype, g, sc, sp, camera_grad,
                                      projector_grad, ws2, s),
                      "backward");
+}
+
+int custma_patch_stats(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                       int32_t kernel_size, int32_t mode, int64_t row_begin, int64_t row_end, double* box,
+                       float* mean, float* sq, float* sqt, const float* shift, float* prep, void* stream) {
+    Geo g;
+    int rc = make_geo(H, W, kernel_size, CUSTMA_LAYOUT_FULL, 0, &g);
+    if (rc || (rc = check_dtype(dtype)) || (rc = set_band(&g, row_begin, row_end))) return rc;
+    if (mode < CUSTMA_STATS_FULL || mode > CUSTMA_STATS_MSB) return fail(CUSTMA_E_ARG, "unknown statistics mode %d", mode);
+    if (g.HV() == 0 || g.W == 0) return CUSTMA_OK;
+    if (!camera || !projector || !box || !mean || !sq || !sqt || (mode == CUSTMA_STATS_BWD_PREP && (!shift || !prep)))
+        return fail(CUSTMA_E_NULL, "null pointer argument");
+    const size_t n = (size_t)H * W;
+    const Stats sc{mean, sq, box, sqt}, sp{mean + n, sq + n, box + n, sqt + n};
+    return check_hip(launch_stats(camera, projector, dtype, g, sc, sp, (hipStream_t)stream, mode, prep, shift,
+                                  STATS_BAND_ROWS),
+                     "patch_stats");
 }
 
 int custma_image_u8_to_unit(const uint8_t* image, int64_t H, int64_t W, int32_t channels, int32_t channel,

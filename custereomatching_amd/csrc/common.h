@@ -364,7 +364,13 @@ struct SideStream {
 // shared, and a wait binds to the most recent record at the time it is enqueued).
 hipError_t side_stream(SideStream* out, std::unique_lock<std::mutex>* lock);
 
-enum StatsMode { STATS_FULL = 0, STATS_BOX = 1, STATS_BWD_PREP = 2, STATS_FWD = 3, STATS_MSB = 4 };
+enum StatsMode {
+    STATS_FULL = CUSTMA_STATS_FULL,
+    STATS_BOX = CUSTMA_STATS_BOX,
+    STATS_BWD_PREP = CUSTMA_STATS_BWD_PREP,
+    STATS_FWD = CUSTMA_STATS_FWD,
+    STATS_MSB = CUSTMA_STATS_MSB
+};
 enum StatsRows { STATS_ALL_ROWS = 0, STATS_BAND_ROWS = 1 };
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
                         int mode = STATS_FULL, float* prep = nullptr, const float* shift = nullptr,

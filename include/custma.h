@@ -123,6 +123,25 @@ int custma_disparity_band(const void* camera, const void* projector, int32_t dty
 int custma_profile_enable(int32_t on);
 int custma_profile_mean_ms(int32_t which, float* ms, int32_t* count);
 
+/* Diagnostics (parity tests): the per-pixel patch statistics every op computes first, for image rows
+ * [row_begin, row_end) of both images (plane 0 = camera, 1 = projector), in `mode`:
+ *   FULL      mean, sq, box, sqt        BOX   box, sqt
+ *   BWD_PREP  box + the fused backward's six prepared fp32 images into prep ([2][3][H][W]: X = centred
+ *             moment, patch mean - shift[i], raw image), given shift[2]
+ *   FWD       sq, box                   MSB   mean, sq, box
+ * mean / sq: the reference's own fp32 patch mean and centred-square chain (stereo_matching_kernel.cu:40-69);
+ * box: fp64 patch sum; sqt: fp64-accurate centred moment rounded to fp32.  Outputs: box [2][H][W] doubles,
+ * mean / sq / sqt [2][H][W] floats (all four non-NULL; fields the mode does not write are left as they are).
+ * No counterpart in the reference (its kernel recomputes them per voxel). */
+#define CUSTMA_STATS_FULL 0
+#define CUSTMA_STATS_BOX 1
+#define CUSTMA_STATS_BWD_PREP 2
+#define CUSTMA_STATS_FWD 3
+#define CUSTMA_STATS_MSB 4
+int custma_patch_stats(const void* camera, const void* projector, int32_t dtype, int64_t H, int64_t W,
+                       int32_t kernel_size, int32_t mode, int64_t row_begin, int64_t row_end, double* box,
+                       float* mean, float* sq, float* sqt, const float* shift, float* prep, void* stream);
+
 /* Image preprocessing before the path (examples/verify.py:138-142, 148): an 8-bit image [H][W][channels]
  * (interleaved, as cv2.imread returns it; channels = 1 for grayscale) -> out[H][W] = image[.][.][channel] / 255,
  * computed as numpy does (float64 division, rounded once to float32; out_dtype CUSTMA_F16 rounds that float32

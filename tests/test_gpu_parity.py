@@ -274,6 +274,27 @@ def test_backward_both_images(gpu, case, layout):
     assert np.abs(gp - rp).max() <= tol_p, np.abs(gp - rp).max() / max(1.0, np.abs(rp).max())
 
 
+@pytest.mark.parametrize("case", BWD_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_D{c[3]}_{c[4]}" for c in BWD_CASES])
+@pytest.mark.parametrize("layout", [FULL, WIN])
+def test_backward_given_volume(gpu, case, layout):
+    """The backward handed the forward's volume (the autograd path) against the fp64 oracle, and equal to
+    the recompute path (cost_volume=None: the volume rebuilt in the workspace, as the forward builds it --
+    the fast sweep up to k = 17, the exact kernel above) bit for bit."""
+    H, W, k, D, kind = case
+    cam, proj = make_pair(H, W, max(D, 1), seed=31, kind=kind)
+    lay, Dl = _layout_args(layout, D)
+    g = _rand_grad(O.volume_shape(H, W, lay, Dl), 7)
+    rc, rp = O.backward_f64(g, cam, proj, k, layout=lay, D=Dl)
+    c, p, gd = _dev(cam, gpu), _dev(proj, gpu), _dev(g, gpu)
+    vol = cm.cost_volume_forward(c, p, D, k, layout, "fast")
+    gc, gp = cm.cost_volume_backward(gd, c, p, k, layout, D, camera_grad=True, projector_grad=True, cost_volume=vol)
+    gc2, gp2 = cm.cost_volume_backward(gd, c, p, k, layout, D, camera_grad=True, projector_grad=True)
+    gc, gp = gc.cpu().numpy(), gp.cpu().numpy()
+    assert np.abs(gc - rc).max() <= 1e-5 * max(1.0, np.abs(rc).max())
+    assert np.abs(gp - rp).max() <= 1e-5 * max(1.0, np.abs(rp).max())
+    assert np.array_equal(gc, gc2.cpu().numpy()) and np.array_equal(gp, gp2.cpu().numpy())
+
+
 @pytest.mark.parametrize("case", [(20, 44, 33, 9, "textured"), (18, 40, 18, 10, "smooth")], ids=["k33", "k18"])
 @pytest.mark.parametrize("layout", [FULL, WIN])
 def test_backward_generic_small_bands(gpu, case, layout, monkeypatch):
