@@ -66,6 +66,10 @@ constexpr int NTYPE = 6;  // partial types: T1c, Am, B (camera) | T1p, Ac, Bp (p
 // chunk has two or more, so segments s and s + 2 never overlap (slot parity).
 constexpr int kSeg = 512;
 constexpr uint32_t kOOB = 0x80000000u;
+// The slot-parity argument (plan_bwd's S = 2 x the max chunk overlap) needs every segment of a
+// multi-segment chunk (>= kSeg / 2 columns) to hold >= k + NLB - 1 columns for the largest sliding k
+// (CUSTMA_SWEEP_KS: 31); a violation would only show at run time as NaN gradients (k_bwd_cover).
+static_assert(kSeg / 2 >= 31 + 64 - 1, "segments too narrow for the slot parity at the largest sliding k");
 
 // Chunk geometry (host and device): diagonals [d0, d0+64); camera columns that carry
 // a valid voxel for some lane: [wlo, whi); pixel columns whose box touches one:

@@ -306,9 +306,26 @@ class _RowBandStereoMatching(torch.autograd.Function):
         return gc, gp, None, None, None, None, None, None
 
 
+# Groups built for a given global H, reused by later calls with the same (group, k, band height, H,
+# device): the collective band check then runs once per such key instead of once per call (its MIN
+# all-reduce and host sync would sit in front of every op's halo exchange).  Only with H given: every
+# rank's key then changes together (H is global and band_bounds fixes each rank's height), so all
+# ranks run the check on the same calls.  A custom split (H=None) checks on every call, or takes rbg=.
+_GROUPS: dict = {}
+
+
 def _group_for(rbg, kernel_size, group, n, H, device):
     if rbg is None:
-        return RowBandGroup(kernel_size, group, n=n, H=H, device=device)
+        if H is None:
+            return RowBandGroup(kernel_size, group, n=n, H=H, device=device)
+        key = (id(group), kernel_size, int(n), int(H), str(device))
+        hit = _GROUPS.get(key)
+        if hit is None or hit.group is not group:
+            hit = RowBandGroup(kernel_size, group, n=n, H=H, device=device)
+            if len(_GROUPS) >= 64:
+                _GROUPS.clear()
+            _GROUPS[key] = hit
+        return hit
     if rbg.k != kernel_size or (rbg.n is not None and rbg.n != n):
         raise ValueError(f"rbg was built for kernel_size {rbg.k} and {rbg.n} rows, called with {kernel_size} / {n}")
     return rbg
