@@ -16,7 +16,10 @@
 // 32).  The k x (32+2r) camera and k x (256+2r) projector strips are staged
 // in LDS once; centred operands are formed on the fly (1 LDS read + 1 sub per
 // operand per MFMA step), which is far below the 64-cycle MFMA issue.
+#include <type_traits>
+
 #include "common.h"
+#include "sweep.h"
 
 namespace custma {
 
@@ -133,10 +136,202 @@ __global__ __launch_bounds__(256) void k_fwd_exact(const T* __restrict__ cam, co
         }
     }
 }
+// Compile-time kernel size (KT <= kExactMaxKT): the same MFMA chain with the tap loop laid out at
+// compile time.  The runtime-k kernel above branches per step on the tap's validity and reads its
+// three operands one after another, each behind an lgkmcnt(0) wait (C3 window k = 19: 17.7 ms, 0.25
+// of the fp32 MFMA rate).  Here two image rows (2 KT taps = KT MFMA steps, the same tap-pair pattern
+// for every row pair) are one unrolled block -- every LDS read is a base VGPR + an immediate offset
+// -- looped over the row pairs (a fully unrolled K^2/2-step loop overflows the instruction cache at
+// k = 31), then the last row of an odd KT; a lane's tap is t = 2 s + (lane >> 5), so a step's pair
+// either stays in one row (the kh = 1 lanes read one column on) or wraps to the next row's column 0
+// (they read one row on, KT - 1 columns back): two per-lane bases cover both.
+// Each wave keeps NT accumulator tiles (the camera operand feeds NT MFMAs): window layouts use 3
+// waves x 3 tiles = 288 projector columns (all 32 + 256 diagonals of a D = 256 window in one
+// workgroup, instead of a second 256-column workgroup for the last 32), the full layout 4 x 2.
+constexpr int kExactMaxKT = 33;
+
+template <typename T, int KT, int NW, int NT>
+__global__ __launch_bounds__(64 * NW) void k_fwd_exact_k(const T* __restrict__ cam, const T* __restrict__ proj,
+                                                         Geo g, Stats sc, Stats sp, float* __restrict__ out,
+                                                         int nWT, int nDC) {
+    constexpr int R0 = KT / 2, NC = 32 * NW * NT, CW = TWX + KT - 1, PW = NC + KT - 1, NTH = 64 * NW;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* camT = lds;              // [KT][CW]
+    float* projT = camT + KT * CW;  // [KT][PW]
+    float* csq = projT + KT * PW;   // [TWX]
+    float* cmn = csq + TWX;         // [TWX]
+    float* psq = cmn + TWX;         // [NC]
+    float* pmn = psq + NC;          // [NC]
+
+    const int64_t b = blockIdx.x;
+    const int dc = (int)(b % nDC);
+    const int wt = (int)((b / nDC) % nWT);
+    const int64_t h = g.h_lo + b / ((int64_t)nDC * nWT);
+    const int64_t w0 = (int64_t)wt * TWX;
+    const int64_t dA = (g.layout == CUSTMA_LAYOUT_WINDOW ? w0 : 0) + (int64_t)dc * NC;
+
+    for (int e = threadIdx.x; e < KT * CW; e += NTH) {
+        const int i = e / CW, x = e % CW;
+        camT[e] = ldpad(cam, g.H, g.W, h + i - R0, w0 + x - R0);
+    }
+    for (int e = threadIdx.x; e < KT * PW; e += NTH) {
+        const int i = e / PW, x = e % PW;
+        projT[e] = ldpad(proj, g.H, g.W, h + i - R0, dA + x - R0);
+    }
+    if (threadIdx.x < TWX) {
+        const int64_t w = w0 + threadIdx.x;
+        const bool ok = w < g.W;
+        csq[threadIdx.x] = ok ? sc.sq[h * g.W + w] : 0.f;
+        cmn[threadIdx.x] = ok ? sc.mean[h * g.W + w] : 0.f;
+    }
+    for (int e = threadIdx.x; e < NC; e += NTH) {
+        const int64_t d = dA + e;
+        const bool ok = d < g.W;
+        psq[e] = ok ? sp.sq[h * g.W + d] : 0.f;
+        pmn[e] = ok ? sp.mean[h * g.W + d] : 0.f;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wl = lane & 31, kh = lane >> 5;
+    const int64_t dW = dA + (int64_t)(32 * NT) * wave;  // the wave's first projector column
+    auto tile_live = [&](int64_t dt) {
+        if (dt >= g.W || w0 >= g.WO) return false;
+        if (g.layout == CUSTMA_LAYOUT_WINDOW) return dt - (w0 + TWX - 1) <= g.D && dt + 31 - w0 >= 0;
+        return true;
+    };
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) any |= tile_live(dW + 32 * q);
+    if (!any) return;
+
+    const float mc = cmn[wl];
+    float mp[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) mp[q] = pmn[32 * NT * wave + 32 * q + wl];
+    // per-lane bases (floats): [0] the pair stays in one row, [1] it wraps to the next row
+    const float* cb0 = camT + wl + kh;
+    const float* cb1 = camT + wl + kh * (CW - KT + 1);
+    const float* pb0 = projT + 32 * NT * wave + wl + kh;
+    const float* pb1 = projT + 32 * NT * wave + wl + kh * (PW - KT + 1);
+
+    f32x16 acc[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[q][e] = 0.f;
+
+    // one MFMA step: taps (2 s', 2 s' + 1) of the block starting at tap row `row0` of the strips;
+    // LAST: the tail row's step whose kh = 1 tap is past the patch (zero operand)
+    // one MFMA step = taps (2 s, 2 s + 1) of the block whose first tap row the bases point at:
+    // fetch() reads its raw operands, mma() centres them and issues the NT MFMAs; the block issues
+    // step s + 1's reads before step s's MFMAs (LDS latency behind the MFMA pipe).  LAST: the tail
+    // row's step whose kh = 1 tap lies past the patch (a zero operand).
+    struct Ops {
+        float a, b[NT];
+    };
+    auto fetch = [&](auto sc_, const float* c0, const float* c1, const float* p0, const float* p1) {
+        constexpr int s = decltype(sc_)::value;
+        constexpr int i0 = (2 * s) / KT, j0 = (2 * s) % KT;
+        constexpr bool WRAP = (2 * s + 1) / KT != i0;
+        constexpr int oc = i0 * CW + j0, op = i0 * PW + j0;
+        Ops o;
+        o.a = (WRAP ? c1 : c0)[oc];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) o.b[q] = (WRAP ? p1 : p0)[op + 32 * q];
+        return o;
+    };
+    auto mma = [&](const Ops& o, auto last_) {
+        float a = o.a - mc;
+        if constexpr (decltype(last_)::value) a = kh ? 0.f : a;
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+            acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, o.b[q] - mp[q], acc[q], 0, 0, 0);
+    };
+    // NS steps of a block, software-pipelined one step deep
+    auto block = [&](auto ns_, auto tail_, const float* c0, const float* c1, const float* p0, const float* p1) {
+        constexpr int NS = decltype(ns_)::value;
+        constexpr bool TAIL = decltype(tail_)::value;
+        Ops cur = fetch(std::integral_constant<int, 0>{}, c0, c1, p0, p1);
+        Unroll<0, NS>::run([&](auto sc_) {
+            constexpr int s = decltype(sc_)::value;
+            Ops nxt = cur;
+            if constexpr (s + 1 < NS) nxt = fetch(std::integral_constant<int, s + 1>{}, c0, c1, p0, p1);
+            mma(cur, std::integral_constant<bool, TAIL && s + 1 == NS>{});
+            cur = nxt;
+            // keep the next step's reads ahead of this step's MFMAs: 1 MFMA, then the reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, NT + 1, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, NT - 1, 0);  // MFMA
+        });
+    };
+    // row pairs (2p, 2p + 1): KT steps each, the same pattern for every pair
+    const float *c0 = cb0, *c1 = cb1, *p0 = pb0, *p1 = pb1;
+#pragma unroll 1
+    for (int p = 0; p < KT / 2; ++p) {
+        block(std::integral_constant<int, KT>{}, std::false_type{}, c0, c1, p0, p1);
+        c0 += 2 * CW; c1 += 2 * CW; p0 += 2 * PW; p1 += 2 * PW;
+    }
+    // the last row of an odd KT: (KT + 1) / 2 steps, the final kh = 1 tap empty
+    if constexpr (KT % 2 == 1) block(std::integral_constant<int, (KT + 1) / 2>{}, std::true_type{}, c0, c1, p0, p1);
+
+    // epilogue: cost = (E + eps) / sqrtf(fmaf(X, Y, eps))   (stereo_matching_kernel.cu:71)
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        const int64_t dt = dW + 32 * q;
+        if (!tile_live(dt)) continue;
+        const int64_t d = dt + wl;
+        const float Y = psq[32 * NT * wave + 32 * q + wl];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int wrow = (e & 3) + 8 * (e >> 2) + 4 * kh;
+            const int64_t w = w0 + wrow;
+            if (!voxel_valid(g, w, d)) continue;
+            const float X = csq[wrow];
+            const float den = sqrtf(__builtin_fmaf(X, Y, kEps));
+            out[voxel_index(g, h, w, d)] = (acc[q][e] + kEps) / den;
+        }
+    }
+}
+
+template <typename T, int KT, int NW, int NT>
+hipError_t launch_exact_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out, hipStream_t s) {
+    constexpr int NC = 32 * NW * NT;
+    const int nWT = (int)cdiv(g.WO, TWX);
+    const int nDC = (int)(g.layout == CUSTMA_LAYOUT_WINDOW ? cdiv(TWX + g.D, NC) : cdiv(g.W, NC));
+    const int64_t blocks = g.HV() * nWT * nDC;
+    const size_t lds = sizeof(float) * (KT * (TWX + KT - 1) + KT * (NC + KT - 1) + 2 * TWX + 2 * NC);
+    hipError_t e = allow_lds(k_fwd_exact_k<T, KT, NW, NT>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_fwd_exact_k<T, KT, NW, NT>), dim3((unsigned)blocks), dim3(64 * NW), lds, s, cam, proj, g,
+                       sc, sp, out, nWT, nDC);
+    return hipGetLastError();
+}
+
+template <typename T, int KT>
+hipError_t exact_k(const void* cam, const void* proj, const Geo& g, Stats sc, Stats sp, float* out, hipStream_t s) {
+    if (g.layout == CUSTMA_LAYOUT_WINDOW)
+        return launch_exact_k<T, KT, 3, 3>((const T*)cam, (const T*)proj, g, sc, sp, out, s);
+    return launch_exact_k<T, KT, 4, 2>((const T*)cam, (const T*)proj, g, sc, sp, out, s);
+}
+
+template <int KT>
+hipError_t exact_dispatch(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, float* out,
+                          hipStream_t s) {
+    if constexpr (KT > kExactMaxKT) {
+        return hipErrorInvalidValue;
+    } else {
+        if (g.k == KT)
+            return dtype == CUSTMA_F16 ? exact_k<__half, KT>(cam, proj, g, sc, sp, out, s)
+                                       : exact_k<float, KT>(cam, proj, g, sc, sp, out, s);
+        return exact_dispatch<KT + 1>(cam, proj, dtype, g, sc, sp, out, s);
+    }
+}
 }  // namespace
 
 hipError_t launch_fwd_exact(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                             float* out, hipStream_t s) {
+    if (g.k <= kExactMaxKT) return exact_dispatch<1>(cam, proj, dtype, g, sc, sp, out, s);
     const int nWT = (int)cdiv(g.WO, TWX);
     const int nDC = (int)(g.layout == CUSTMA_LAYOUT_WINDOW ? cdiv(TWX + g.D, TDX) : cdiv(g.W, TDX));
     const int64_t blocks = g.HV() * nWT * nDC;
