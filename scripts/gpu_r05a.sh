@@ -10,6 +10,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
+md5sum custereomatching_amd/_lib/libcustma_hip.so
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit $1;; esac; }
 timeout -k 10 400 python -u scripts/diag_bwd.py --all > $O/diag_bwd.log 2>&1
 rc=$?; echo "diag rc=$rc"; fatal $rc diag
