@@ -69,7 +69,9 @@ int set_band(Geo* g, int64_t row_begin, int64_t row_end) {
     return CUSTMA_OK;
 }
 
-size_t stats_bytes(const Geo& g) { return 2 * align256((size_t)g.H * g.W * 20); }
+// the two images' statistics, then the fused forward's per-band counters (bands of >= 8 rows)
+size_t stats_bytes(const Geo& g) { return 2 * align256((size_t)g.H * g.W * 20) + align256(4 * (size_t)(g.H / 8 + 1)); }
+int* band_counters(const Geo& g, void* ws) { return (int*)((char*)ws + 2 * align256((size_t)g.H * g.W * 20)); }
 
 size_t volume_bytes(const Geo& g) { return (size_t)g.HV() * g.WO * g.DO * sizeof(float); }
 
@@ -316,6 +318,12 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
     const bool fast = precision == CUSTMA_FAST && fast_supported(g.k) && g.k <= kFastVolumeMaxK;
+    // the statistics pass fused into the sweep's launch (large window volumes)
+    if (fast && fused_forward_ok(g, cost_volume)) {
+        carve_stats(g, workspace, &sc, &sp);
+        return check_hip(launch_fwd_fused(camera, projector, dtype, g, sc, sp, cost_volume, band_counters(g, workspace), s),
+                         "forward(fused)");
+    }
     // (eager calls only: under stream capture the single-stream form is recorded)
     if (fast && split_forward(g) && stream_on_current_device(s)) {
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

@@ -267,22 +267,28 @@ __device__ __forceinline__ void asm_ld_img4(uint32_t& pe0, uint32_t& pe1, uint32
             : "v"(vP0), "v"(vP1), "s"(dP), "s"(sE), "s"(sL));
     }
 }
+// SC1: the loads bypass this CU's L1 (`sc1`, L2-served): statistics written in the same launch by other
+// workgroups with write-through stores (the fused forward, sweep_wave.hip)
+#define CUSTMA_LD_STAT6(POL)                                                                                  \
+    asm volatile("s_nop 4\n\t"                                                                               \
+                 "buffer_load_dwordx2 %0, %6, %12, %16 offen" POL "\n\t"                                     \
+                 "buffer_load_dwordx2 %1, %7, %12, %16 offen" POL "\n\t"                                     \
+                 "buffer_load_dword %2, %8, %13, %17 offen" POL "\n\t"                                       \
+                 "buffer_load_dword %3, %9, %13, %17 offen" POL "\n\t"                                       \
+                 "buffer_load_dwordx2 %4, %10, %14, %16 offen" POL "\n\t"                                    \
+                 "buffer_load_dword %5, %11, %15, %17 offen" POL                                               \
+                 : "=&v"(m0), "=&v"(m1), "=&v"(q0), "=&v"(q1), "=&v"(ub), "=&v"(uq)                            \
+                 : "v"(vM0), "v"(vM1), "v"(vQ0), "v"(vQ1), "v"(vUB), "v"(vUQ), "s"(dPB), "s"(dPS), "s"(dCB), \
+                   "s"(dCS), "s"(s8), "s"(s4))
+template <bool SC1 = false>
 __device__ __forceinline__ void asm_ld_stat6(double& m0, double& m1, uint32_t& q0, uint32_t& q1, double& ub,
                                              uint32_t& uq, uint32_t vM0, uint32_t vM1, uint32_t vQ0, uint32_t vQ1,
                                              uint32_t vUB, uint32_t vUQ, i32x4 dPB, i32x4 dPS, i32x4 dCB, i32x4 dCS,
                                              uint32_t s8, uint32_t s4) {
-    asm volatile(
-        "s_nop 4\n\t"
-        "buffer_load_dwordx2 %0, %6, %12, %16 offen\n\t"
-        "buffer_load_dwordx2 %1, %7, %12, %16 offen\n\t"
-        "buffer_load_dword %2, %8, %13, %17 offen\n\t"
-        "buffer_load_dword %3, %9, %13, %17 offen\n\t"
-        "buffer_load_dwordx2 %4, %10, %14, %16 offen\n\t"
-        "buffer_load_dword %5, %11, %15, %17 offen"
-        : "=&v"(m0), "=&v"(m1), "=&v"(q0), "=&v"(q1), "=&v"(ub), "=&v"(uq)
-        : "v"(vM0), "v"(vM1), "v"(vQ0), "v"(vQ1), "v"(vUB), "v"(vUQ), "s"(dPB), "s"(dPS), "s"(dCB), "s"(dCS),
-          "s"(s8), "s"(s4));
+    if constexpr (SC1) CUSTMA_LD_STAT6(" sc1");
+    else CUSTMA_LD_STAT6("");
 }
+#undef CUSTMA_LD_STAT6
 __device__ __forceinline__ void asm_ld_f64(double& d, uint32_t off, i32x4 r) {
     asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(d) : "v"(off), "s"(r));
 }

@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "stats_body.h"
 #include "sweep.h"
 
 // Build: compiled once per kernel size with -DCUSTMA_SW_K=<k> (the kernels and launchers of
@@ -74,7 +75,7 @@ constexpr int kFwdPF = 2;  // outputs whose projector statistics are read ahead 
 // instead of four 16-address loads per wave and step: those loads were most of the sweep's load
 // cost (C5: 9.80 -> 8.25 ms with every camera load out of range, profiles/r03/fwdabl).
 template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2, int AMX_ = 0,
-          bool CPL = false>
+          bool CPL = false, bool SC1 = false>
 __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
                                           const Stats& sc, const Stats& sp, float* __restrict__ out,
                                           int64_t u0, int64_t h0, int64_t h1, int64_t d0,
@@ -160,7 +161,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             if constexpr (C3R) asm_ld_img2<T>(p.ce2, p.cl2, vC2, dCam, sE, sL);
         }
         const bool st = ti >= h0i && ti < h1i;
-        asm_ld_stat6(p.m0, p.m1, p.q0, p.q1, p.ub, p.uq, vM0, vM1, vQ0, vQ1, vUB, vUQ, dPB, dPS, dCB, dCS,
+        asm_ld_stat6<SC1>(p.m0, p.m1, p.q0, p.q1, p.ub, p.uq, vM0, vM1, vQ0, vQ1, vUB, vUQ, dPB, dPS, dCB, dCS,
                      so_row(ti, rb8, st), so_row(ti, rb4, st));
     };
     auto tie = [&](Stage& p) {
@@ -505,13 +506,79 @@ __global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, cons
 constexpr int kTileP = 2;  // load pipeline depth (steps; 3 measured no faster)
 constexpr int kWaveLds = (3 * kRowP + 64) * 8 + kRowP * 4;  // rowE, rowL, sM, sR (f64) + sQ (f32)
 
-template <int K, typename T, bool X4, int AMX = 0, bool CPL = false>
+// FUSED (the statistics pass in the same launch; window layout, four chunks, 64-row bands): a
+// workgroup is either a STATISTICS tile (stats_body.h: 32 columns x 64 rows of one image, mode
+// STATS_FWD, stored write-through) or a SWEEP tile.  Each XCD (hardware block b runs on XCD b % 8,
+// the observed round-robin) walks its own contiguous range of bands in the order
+//     S(b0) S(b1) [T(b0) S(b2)] [T(b1) S(b3)] ... T(b_last)
+// (S(b): the band's nSC x 2 statistics tiles, T(b): its nTile sweep tiles), so the statistics of band
+// b + 2 run beside the sweeps of band b instead of as a separate pass in front of the whole sweep.
+// A statistics tile counts itself into cnt[band] (agent-scope atomic add after every storing wave's
+// `s_waitcnt vmcnt(0)` and a barrier); a sweep tile's first lane polls cnt[band] (`sc1` load) until
+// all of the band's tiles have counted, and the sweep reads the statistics with `sc1` loads (L1
+// bypassed, served by L2 / memory; the rows are whole 128-byte lines, W % 32 == 0).  A sweep tile
+// waits only for tiles of LOWER hardware index, so the grid cannot deadlock whatever the placement
+// (blocks start in index order); the poll is bounded, never a hang.
+constexpr int kFusedMinK = 3;
+struct FusedGrid {
+    int nBand, nTile, nSC, P, perX, len;  // P = 2 nSC statistics tiles per band; perX bands per XCD
+};
+
+template <int K, typename T, bool X4, int AMX = 0, bool CPL = false, bool FUSED = false>
 __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __restrict__ cam,
                                                                  const T* __restrict__ proj, Geo g, Stats sc,
                                                                  Stats sp, float* __restrict__ out, WaveGrid wg,
-                                                                 DispPartial part) {
+                                                                 DispPartial part, int* cnt = nullptr,
+                                                                 FusedGrid fg = FusedGrid{}) {
     extern __shared__ __attribute__((aligned(16))) double lds_t[];
     const int w = (int)(threadIdx.x >> 6);
+    int wt, band;
+    if constexpr (FUSED) {
+        const int x = (int)(blockIdx.x % 8), j0 = (int)(blockIdx.x / 8);
+        const int blo = x * fg.perX, m = min(fg.perX, fg.nBand - blo);
+        if (m <= 0) return;
+        int j = j0, sb = -1, si = 0;
+        wt = -1;
+        band = 0;
+        const int pre = min(2, m) * fg.P;
+        if (j < pre) {
+            sb = blo + j / fg.P;
+            si = j % fg.P;
+        } else {
+            j -= pre;
+            const int G = fg.nTile + fg.P, full = max(0, m - 2);
+            if (j < full * G) {
+                const int gi = j / G, r = j % G;
+                if (r < fg.nTile) { band = blo + gi; wt = r; }
+                else { sb = blo + gi + 2; si = r - fg.nTile; }
+            } else {
+                j -= full * G;
+                const int gi = full + j / fg.nTile;
+                if (gi >= m) return;
+                band = blo + gi;
+                wt = j % fg.nTile;
+            }
+        }
+        if (sb >= 0) {  // statistics tile: image si / nSC, column tile si % nSC, row tile sb
+            stats_detail::stats_tile<T, K, STATS_FWD, true>(cam, proj, g, sc, sp, nullptr, nullptr, g.h_lo, g.h_hi,
+                                                           si % fg.nSC, sb, si / fg.nSC, lds_t);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores are out
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + sb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        if (threadIdx.x == 0) {  // wait for the band's statistics (bounded: ~0.5 s, then go on)
+            for (int it = 0; it < (1 << 20); ++it) {
+                if (__hip_atomic_load(cnt + band, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= fg.P) break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        __syncthreads();
+    } else {
+        const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
+        wt = (int)(bid % wg.nTile);
+        band = (int)(bid / wg.nTile);
+    }
     char* mine = (char*)lds_t + w * kWaveLds;
     double* rowE = (double*)mine;
     double* rowL = rowE + kRowP;
@@ -520,9 +587,6 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     float* sQ = (float*)(sR + 64);
     float* stage = (float*)((char*)lds_t + wg.nChunk * kWaveLds);
     T* camL = (T*)(stage + 2 * TW * g.DO);  // CPL: the camera block after the two stage buffers
-    const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int wt = (int)(bid % wg.nTile);
-    const int band = (int)(bid / wg.nTile);
     const int64_t u0 = (int64_t)wt * TW;
     const int64_t h0 = g.h_lo + (int64_t)band * wg.TH, h1 = min(g.h_hi, h0 + wg.TH);
     const int64_t d0 = (int64_t)w * 64;
@@ -531,14 +595,14 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
     constexpr int kTP = X4 ? kTileP : 2;  // deeper pipelines only with the 16-byte stores (vmcnt range)
     if (!wg.rem)
-        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL,
-                                                                  sM, sQ, sR, stage, part, camL);
+        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+                                                                         rowL, sM, sQ, sR, stage, part, camL);
     else if (w == wg.nChunk - 1)
-        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL,
-                                                                 sM, sQ, sR, stage, part, camL);
+        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+                                                                        rowL, sM, sQ, sR, stage, part, camL);
     else
-        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE, rowL,
-                                                                  sM, sQ, sR, stage, part, camL);
+        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+                                                                         rowL, sM, sQ, sR, stage, part, camL);
 }
 
 // CPL: fp16 images, when the camera block keeps the tile kernel at three workgroups per CU (LDS
@@ -588,6 +652,48 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
     return hipGetLastError();
 }
 
+// The fused forward (statistics + sweep in one launch, FusedGrid; the caller checked fused_forward_ok()):
+// cnt (nBand ints of workspace) is zeroed on the stream before the launch.
+template <int K, typename T>
+hipError_t launch_fused(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out, int* cnt,
+                        hipStream_t s) {
+    if constexpr (K < kFusedMinK) {  // (the statistics body at k <= 2 keeps a small array in scratch)
+        return hipErrorInvalidValue;
+    } else {
+    const WaveGrid wg = wave_grid(g);
+    if (wg.nChunk != kTileMaxChunks || wg.TH != 64) return hipErrorInvalidValue;
+    FusedGrid fg;
+    fg.nBand = wg.nBand;
+    fg.nTile = wg.nTile;
+    fg.nSC = (int)cdiv(g.W, 32);
+    fg.P = 2 * fg.nSC;
+    fg.perX = (int)cdiv(wg.nBand, 8);
+    const int m = fg.perX;  // the longest per-XCD sequence (XCD 0 holds perX bands)
+    fg.len = min(2, m) * fg.P + max(0, m - 2) * (fg.nTile + fg.P) + min(2, m) * fg.nTile;
+    size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
+    const bool cpl = cpl_ok<K, T>(g, wg, lds);
+    if (cpl) lds += cpl_bytes<K, T>(wg);
+    lds = std::max(lds, stats_detail::stats_lds_bytes(STATS_FWD, K));
+    hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)fg.nBand, s);
+    if (e != hipSuccess) return e;
+    const dim3 grid((unsigned)(8 * (int64_t)fg.len)), blk(64 * wg.nChunk);
+    prof_begin(PROF_FWD, s);
+    if (cpl) {
+        if constexpr (sizeof(T) == 2) {
+            if ((e = allow_lds(k_fwd_tile<K, T, true, 0, true, true>, lds)) != hipSuccess) return e;
+            hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, true, true>), grid, blk, lds, s, cam, proj, g, sc, sp, out, wg,
+                               DispPartial{}, cnt, fg);
+        }
+    } else {
+        if ((e = allow_lds(k_fwd_tile<K, T, true, 0, false, true>, lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, false, true>), grid, blk, lds, s, cam, proj, g, sc, sp, out, wg,
+                           DispPartial{}, cnt, fg);
+    }
+    prof_end(PROF_FWD, s);
+    return hipGetLastError();
+    }
+}
+
 // Fused disparity through the tile kernel (window layout, D + 1 <= 257): one partial per pixel.
 template <int K, typename T>
 hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, DispPartial part, hipStream_t s) {
@@ -618,6 +724,13 @@ hipError_t sw_fwd(const void* cam, const void* proj, int dtype, const Geo& g, St
     return launch_k<K, float>((const float*)cam, (const float*)proj, g, sc, sp, out, s);
 }
 template <int K>
+hipError_t sw_fwd_fused(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, float* out,
+                        int* cnt, hipStream_t s) {
+    if (dtype == CUSTMA_F16)
+        return launch_fused<K, __half>((const __half*)cam, (const __half*)proj, g, sc, sp, out, cnt, s);
+    return launch_fused<K, float>((const float*)cam, (const float*)proj, g, sc, sp, out, cnt, s);
+}
+template <int K>
 hipError_t sw_amx(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, DispPartial part,
                   hipStream_t s) {
     if (dtype == CUSTMA_F16) return launch_amx<K, __half>((const __half*)cam, (const __half*)proj, g, sc, sp, part, s);
@@ -625,6 +738,8 @@ hipError_t sw_amx(const void* cam, const void* proj, int dtype, const Geo& g, St
 }
 #ifdef CUSTMA_SW_K
 template hipError_t sw_fwd<CUSTMA_SW_K>(const void*, const void*, int, const Geo&, Stats, Stats, float*, hipStream_t);
+template hipError_t sw_fwd_fused<CUSTMA_SW_K>(const void*, const void*, int, const Geo&, Stats, Stats, float*, int*,
+                                              hipStream_t);
 template hipError_t sw_amx<CUSTMA_SW_K>(const void*, const void*, int, const Geo&, Stats, Stats, DispPartial,
                                         hipStream_t);
 #endif
@@ -658,6 +773,26 @@ hipError_t launch_disp_tile(const void* cam, const void* proj, int dtype, const 
     switch (g.k) {
 #define CUSTMA_K(KK) \
     case KK: return sw_amx<KK>(cam, proj, dtype, g, sc, sp, part, s);
+        CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+        default: return hipErrorInvalidValue;
+    }
+}
+
+bool fused_forward_ok(const Geo& g, const void* out) {
+    const char* e = getenv("CUSTMA_FWD_FUSED");  // 0: separate statistics pass (same-box A/B)
+    if (e && e[0] == '0') return false;
+    if (g.layout != CUSTMA_LAYOUT_WINDOW || g.W % 32 != 0 || g.band_rows > 0 || g.k < 3) return false;
+    const WaveGrid wg = wave_grid(g);
+    const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0);
+    return x4 && wg.nChunk == kTileMaxChunks && wg.TH == 64 && g.HV() >= 8 * 64;
+}
+
+hipError_t launch_fwd_fused(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
+                            float* out, int* cnt, hipStream_t s) {
+    switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: return sw_fwd_fused<KK>(cam, proj, dtype, g, sc, sp, out, cnt, s);
         CUSTMA_SWEEP_KS(CUSTMA_K)
 #undef CUSTMA_K
         default: return hipErrorInvalidValue;

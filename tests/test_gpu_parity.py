@@ -575,9 +575,10 @@ def _split_inputs(gpu):
     return _dev(cam, gpu, torch.float16), _dev(proj, gpu, torch.float16), H, D, k
 
 
-def test_split_forward_matches_half_bands(gpu):
+def test_split_forward_matches_half_bands(gpu, monkeypatch):
     """The two-stream forward equals the same rows computed as two separate band calls (each below the
     split size), bit for bit, and stays within the fast tolerance of the exact volume."""
+    monkeypatch.setenv("CUSTMA_FWD_FUSED", "0")
     c, p, H, D, k = _split_inputs(gpu)
     full = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
     torch.cuda.synchronize()
@@ -595,9 +596,10 @@ def test_split_forward_matches_half_bands(gpu):
         assert float((ex - full[h0:h0 + 8]).abs().max()) <= O.fast_tolerance(k)
 
 
-def test_split_forward_graph_capture(gpu):
+def test_split_forward_graph_capture(gpu, monkeypatch):
     """Under stream capture the forward records its single-stream form (capi.hip: the side-stream
     split is for eager calls): a replay on new inputs equals the eager (split) forward bit for bit."""
+    monkeypatch.setenv("CUSTMA_FWD_FUSED", "0")
     c, p, H, D, k = _split_inputs(gpu)
     out = torch.empty(H, c.shape[1] - D, D + 1, device=gpu)
     side = torch.cuda.Stream(gpu)
@@ -617,3 +619,52 @@ def test_split_forward_graph_capture(gpu):
     torch.cuda.synchronize(gpu)
     ref = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
     assert torch.equal(out, ref)
+
+
+# ---- the fused forward (sweep_wave.hip k_fwd_tile FUSED): the statistics tiles run in the sweep's own
+# launch, each band's sweep tiles waiting on a per-band counter (large window volumes, 64-row bands) ----
+
+FUSED_CASES = [
+    (1280, 2048, 256, 11, torch.float16),  # C3-like: D = 256, four chunks + the remainder diagonal
+    (1216, 2048, 200, 4, torch.float16),   # no remainder diagonal; even k
+    (1280, 2048, 250, 16, torch.float32),  # fp32 images, the largest even sliding k
+    (1344, 2080, 256, 3, torch.float16),   # 2080 % 32 == 0, k = 3 (the smallest fused k)
+]
+
+
+@pytest.mark.parametrize("case", FUSED_CASES, ids=[f"{c[0]}x{c[1]}_D{c[2]}_k{c[3]}" for c in FUSED_CASES])
+def test_fused_forward_matches_separate_statistics(gpu, monkeypatch, case):
+    """The fused launch writes the volume bit for bit as the separate statistics pass + sweep do, also
+    when replayed from a hipGraph; sampled rows stay within the fast tolerance of the exact volume."""
+    H, W, D, k, dt = case
+    cam, proj = make_pair(H, W, D, seed=71)
+    c, p = _dev(cam, gpu, dt), _dev(proj, gpu, dt)
+    fused = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
+    monkeypatch.setenv("CUSTMA_FWD_FUSED", "0")
+    monkeypatch.setenv("CUSTMA_FWD_SPLIT", "0")
+    sep = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
+    torch.cuda.synchronize()
+    assert torch.equal(fused, sep)
+    del sep
+    monkeypatch.delenv("CUSTMA_FWD_FUSED")
+    monkeypatch.delenv("CUSTMA_FWD_SPLIT")
+    out = torch.empty_like(fused)
+    s = torch.cuda.Stream(gpu)
+    s.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(s):
+        cm.cost_volume_forward(c, p, D, k, WIN, "fast", out=out)
+    torch.cuda.current_stream(gpu).wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    out.zero_()
+    with torch.cuda.graph(graph):
+        cm.cost_volume_forward(c, p, D, k, WIN, "fast", out=out)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, fused)
+    del out, graph
+    r0, r1 = k // 2, k - 1 - k // 2
+    for h0 in (0, 64 * 7 - 3, H - 8):
+        a0 = max(0, h0 - r0)
+        ex = cm.cost_volume_forward(c[a0:h0 + 8 + r1].contiguous(), p[a0:h0 + 8 + r1].contiguous(), D, k, WIN,
+                                    "exact", rows=(h0 - a0, h0 - a0 + 8))
+        assert float((ex - fused[h0:h0 + 8]).abs().max()) <= O.fast_tolerance(k), h0

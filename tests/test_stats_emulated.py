@@ -45,6 +45,7 @@ def emu(tmp_path_factory):
     shim = open(os.path.join(HERE, "emu", "shim", "common.h")).read().replace("@EMU_DECLS@", _decls())
     (d / "common.h").write_text(shim)
     shutil.copy(os.path.join(HERE, "emu", "shim", "sweep.h"), d / "sweep.h")
+    shutil.copy(os.path.join(CSRC, "stats_body.h"), d / "stats_body.h")
     shutil.copy(os.path.join(ROOT, "include", "custma.h"), d / "custma.h")
     src = open(os.path.join(CSRC, "stats.hip")).read()
     lds = re.search(r"extern __shared__[^;]*double lds_d\[\];", src)
