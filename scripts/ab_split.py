@@ -1,6 +1,8 @@
-"""Same-process interleaved A/B of the split forward (capi.hip forward_split) against the
-single-stream form (CUSTMA_FWD_SPLIT=0, read per call): forward op time (HIP events around the op)
-at C3 and C5 window.  Usage: python scripts/ab_split.py [rounds]"""
+"""Same-process interleaved A/B/C of the forward's three forms at C3 and C5 window: the fused launch
+(statistics tiles inside the sweep's grid, the default), the split forward (CUSTMA_FWD_FUSED=0: two
+half-band sweeps on two streams) and the single stream (CUSTMA_FWD_FUSED=0 CUSTMA_FWD_SPLIT=0); both
+switches are read per call.  Forward op time from HIP events around the op; every form's volume must
+equal the first one's bit for bit.  Usage: python scripts/ab_split.py [rounds]"""
 import json
 import os
 import statistics
@@ -13,6 +15,8 @@ import custereomatching_amd as cm  # noqa: E402
 from bench import EventTimer, synth_pair  # noqa: E402
 from kbench import CFGS, warm  # noqa: E402
 
+FORMS = {"fused": {}, "split": {"CUSTMA_FWD_FUSED": "0"},
+         "single": {"CUSTMA_FWD_FUSED": "0", "CUSTMA_FWD_SPLIT": "0"}}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 for name in ("c3_win", "c5_win"):
     c = CFGS[name]
@@ -20,22 +24,27 @@ for name in ("c3_win", "c5_win"):
     cam, proj = synth_pair(H, W, D, 5, "cuda", dt)
     out = cm.cost_volume_forward(cam, proj, D, k, lay, "fast")
     ref = out.clone()
-    res = {"1": [], "0": []}
+    res = {f: [] for f in FORMS}
     reps = 20 if name == "c3_win" else 6
     for r in range(rounds):
-        for mode in ("1", "0"):
-            os.environ["CUSTMA_FWD_SPLIT"] = mode
+        for form, env in FORMS.items():
+            for key in ("CUSTMA_FWD_FUSED", "CUSTMA_FWD_SPLIT"):
+                os.environ.pop(key, None)
+            os.environ.update(env)
             warm(lambda: cm.cost_volume_forward(cam, proj, D, k, lay, "fast", out=out))
             et = EventTimer()
             for _ in range(reps):
                 et.record(lambda: cm.cost_volume_forward(cam, proj, D, k, lay, "fast", out=out))
-            res[mode].append(et.mean_ms())
-            assert torch.equal(out, ref), "split and single-stream volumes differ"
+            res[form].append(et.mean_ms())
+            assert torch.equal(out, ref), f"{form}: volume differs"
+    for key in ("CUSTMA_FWD_FUSED", "CUSTMA_FWD_SPLIT"):
+        os.environ.pop(key, None)
     nb = out.numel() * 4 + 2 * H * W * cam.element_size()
-    print(json.dumps({"cfg": name, "split_ms": [round(x, 4) for x in res["1"]],
-                      "single_ms": [round(x, 4) for x in res["0"]],
-                      "split_median": round(statistics.median(res["1"]), 4),
-                      "single_median": round(statistics.median(res["0"]), 4),
-                      "single_frac_of_8TBps": round(nb / statistics.median(res["0"]) / 1e6 / 8000, 4)}), flush=True)
+    line = {"cfg": name}
+    for form in FORMS:
+        med = statistics.median(res[form])
+        line[form] = {"ms": [round(x, 4) for x in res[form]], "median_ms": round(med, 4),
+                      "frac_of_8TBps": round(nb / med / 1e6 / 8000, 4)}
+    print(json.dumps(line), flush=True)
     del out, ref
     torch.cuda.empty_cache()
