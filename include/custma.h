@@ -13,7 +13,8 @@
  * custma_workspace_bytes(...) bytes, owned by the caller (the torch caching
  * allocator in the Python shim); no device memory is allocated inside a call
  * and nothing synchronises the host.  Work runs on `stream`, except that an
- * eager (not capturing) fast window forward of >= 1 GB forks its second half
+ * eager (not capturing) fast window forward of >= 1 GB that does not take the
+ * fused form (statistics tiles inside the sweep's launch) forks its second half
  * onto a per-device side stream the library creates once, and makes `stream`
  * wait for it before returning (stream order is unchanged).  Under capture
  * every call stays on `stream`, so every call is hipGraph-capturable
@@ -59,10 +60,11 @@ extern "C" {
 #define CUSTMA_E_LAUNCH (-4)    /* HIP launch / runtime error */
 #define CUSTMA_E_UNSUPPORTED (-5)
 
-/* kernel_size range.  Odd k <= 17 run the sliding-window (fast) kernels; every other size -- odd k up to
- * CUSTMA_MAX_KERNEL and even k, whose taps sit at offsets -k/2 .. k-1-k/2 exactly as the reference's
- * `kernel_size / 2` origin (stereo_matching_kernel.cu:44,60) -- runs the exact forward and the generic
- * fp64 backward. */
+/* kernel_size range.  Even k has its taps at offsets -k/2 .. k-1-k/2, exactly as the reference's
+ * `kernel_size / 2` origin (stereo_matching_kernel.cu:44,60).  Every k <= 17 and odd k <= 31 run the
+ * sliding-window kernels (fused backward, fused disparity; the fast volume up to k = 17, the exact one
+ * above -- capi.hip kFastVolumeMaxK); the exact forward has compile-time instantiations up to k = 33;
+ * other sizes up to CUSTMA_MAX_KERNEL run the runtime-k exact forward and the generic fp64 backward. */
 #define CUSTMA_MAX_KERNEL 63
 
 int custma_abi_version(void); /* 2 */
@@ -88,7 +90,9 @@ int custma_forward(const void* camera, const void* projector, int32_t dtype, int
  * stereo_matching_backward_wrapper + get_patches_grad_kernel + patches_grad_to_image_kernel
  * (custma/src/stereo_matching_kernel.cu:75-179, :218-261).  Deterministic (no atomics).
  * `cost_volume` is the forward's output for the same images (the autograd op keeps it); NULL makes
- * the call recompute it into the workspace (size the workspace with CUSTMA_OP_BACKWARD_RECOMPUTE).
+ * the call recompute it into the workspace exactly as custma_forward(precision FAST) returns it (the
+ * sliding fp64 volume up to k = 17, the exact one above; size the workspace with
+ * CUSTMA_OP_BACKWARD_RECOMPUTE).
  * Window layouts with D = 64 n recompute the last diagonal's cost from the images rather than read
  * it (one 128-byte line per voxel saved), as the reference recomputes every voxel's cost.
  * camera_grad / projector_grad may each be NULL (not computed); the reference computes the
