@@ -785,7 +785,7 @@ bool fused_forward_ok(const Geo& g, const void* out) {
     if (g.layout != CUSTMA_LAYOUT_WINDOW || g.W % 32 != 0 || g.band_rows > 0 || g.k < 3) return false;
     const WaveGrid wg = wave_grid(g);
     const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0);
-    return x4 && wg.nChunk == kTileMaxChunks && wg.TH == 64 && g.HV() >= 8 * 64;
+    return x4 && wg.nChunk == kTileMaxChunks && wg.TH == 64 && wg.nBand >= 8;  // every XCD holds a band
 }
 
 hipError_t launch_fwd_fused(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
