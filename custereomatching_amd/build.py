@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libcustma_hip.so")
 SOURCES = ["capi.hip", "stats.hip", "fwd_exact.hip", "sweep_fwd.hip", "sweep_wave.hip", "bwd_fused.hip", "bwd_generic.hip", "select.hip", "preprocess.hip"]
-SWEEP_KS = tuple(range(1, 18)) + tuple(range(19, 32, 2))  # CUSTMA_SWEEP_KS in csrc/sweep.h
+SWEEP_KS = tuple(range(1, 32))  # CUSTMA_SWEEP_KS in csrc/sweep.h
 # translation units: (object name, source, defines).  sweep_wave.hip compiles once per kernel
 # size (its instantiations dominate the build) plus once for the dispatch.
 UNITS = [(os.path.splitext(src)[0], src, []) for src in SOURCES if src != "sweep_wave.hip"]

@@ -96,10 +96,11 @@ __device__ __forceinline__ void fin_bc(double& e, float& den2, double s, double 
 }
 
 // Kernel sizes with a compile-time sweep instantiation (register-resident
-// column sums need a static trip count): every k <= 17 and odd k <= 31 (the
-// backward's K-deep ring of 16 rows fills the CU's LDS at 31).  Other sizes up
-// to CUSTMA_MAX_KERNEL run on the exact forward and the generic fp64 backward.
-#define CUSTMA_SWEEP_KS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(19) X(21) X(23) X(25) X(27) X(29) X(31)
+// column sums need a static trip count): every k <= 31 (round 5: even k 18 .. 30 too; the
+// backward's K-deep ring of 16 rows fills the CU's LDS at 31, the forward's 16 + k - 1 camera
+// columns its three broadcast registers at 33).  Other sizes up to CUSTMA_MAX_KERNEL run on the
+// exact forward and the generic fp64 backward.
+#define CUSTMA_SWEEP_KS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
 
 struct SweepGrid {
     int nChunk;  // diagonal chunks per column tile

@@ -141,12 +141,12 @@ def test_config2_forward_backward_full_size(gpu, layout, D):
 
 # ---------------- k > 17 (generic fp64 backward) and even k (fused sweep) at a mid size ----------------
 
-@pytest.mark.parametrize("layout,D,k", [("window", 64, 18), ("full", 0, 33), ("window", 64, 16), ("full", 0, 12),
-                                        ("window", 128, 25)])
+@pytest.mark.parametrize("layout,D,k", [("window", 64, 34), ("full", 0, 33), ("window", 64, 16), ("full", 0, 12),
+                                        ("window", 128, 25), ("window", 64, 18)])
 def test_generic_backward_mid_size(gpu, layout, D, k):
-    """Mid-size problems: k = 18, 33 through the banded generic backward (grid-stride kernels, bounded
+    """Mid-size problems: k = 33, 34 through the banded generic backward (grid-stride kernels, bounded
     workspace; the 512 x 512 full layout takes two bands of output rows at the default 2 GiB band
-    budget), k = 12, 16, 25 through the fused sweep; checked on haloed oracle bands."""
+    budget), k = 12, 16, 18, 25 through the fused sweep; checked on haloed oracle bands."""
     H = W = 1024 if layout == "window" else 512
     o = k // 2
     cam, proj = make_pair(H, W, max(D, 1), seed=85)
@@ -233,10 +233,11 @@ def test_config4_window_fp16_one_gpu(gpu):
 
 # ---------------- kernel sizes beyond the fused instantiations (generic paths) ----------------
 
-@pytest.mark.parametrize("k", [33, 35, 18, 20])
+@pytest.mark.parametrize("k", [33, 35, 34, 18, 20, 30])
 def test_large_and_even_kernel_sizes_through_autograd(gpu, k):
-    """k = 33, 35, 18, 20 (above the sliding instantiations; even k with the reference's
-    kernel_size / 2 origin): exact forward + generic fp64 backward via the op."""
+    """k = 33, 34, 35 (above the sliding instantiations: exact forward + generic fp64 backward) and even
+    k = 18, 20, 30 (the reference's kernel_size / 2 origin; sliding backward and disparity, exact
+    volume) via the op."""
     H, W, D = 28, 60, 12
     cam, proj = make_pair(H, W, D, seed=200 + k)
     for layout in ("full", "window"):
@@ -257,9 +258,9 @@ def test_large_and_even_kernel_sizes_through_autograd(gpu, k):
         assert np.array_equal(idx.cpu().numpy(), ridx)
 
 
-@pytest.mark.parametrize("k", [2, 4, 8, 16, 19, 25, 31])
+@pytest.mark.parametrize("k", [2, 4, 8, 16, 19, 22, 25, 28, 31])
 def test_sliding_kernel_sizes_through_autograd(gpu, k):
-    """Even k (taps -k/2 .. k/2-1, stereo_matching_kernel.cu:44,60) and odd k up to 31 on the sliding kernels:
+    """Even k (taps -k/2 .. k/2-1, stereo_matching_kernel.cu:44,60) and every k up to 31 on the sliding kernels:
     fast forward within the cost bound (k <= 17; larger k write the exact volume), fused backward of
     both images within 1e-5, certified disparity (sliding partials) bit-identical to the exact
     volume's argmax."""

@@ -57,7 +57,8 @@ CASES = [
     (17, 33, 10, 6, "smooth"),
     (21, 50, 2, 11, "textured"),
     (26, 70, 16, 24, "quantized"),  # the largest even sliding instantiation (16 + 15 = 31 columns)
-    (19, 45, 18, 9, "textured"),   # even k beyond the sliding instantiations: exact kernel only
+    (19, 45, 18, 9, "textured"),   # even k > 17: sliding kernels (round 5), the exact volume
+    (19, 80, 34, 9, "textured"),   # even k beyond the sliding instantiations: exact kernel only
     (12, 70, 33, 20, "textured"),  # beyond the sliding instantiations: exact kernel only
     (24, 48, 5, 16, "constant"),
     (24, 48, 5, 16, "zeros"),
@@ -172,7 +173,8 @@ DISP_CASES = [
     (24, 64, 17, 20, "textured"),  # the largest sweep instance
     (20, 40, 4, 12, "textured"),   # even k (sliding kernels)
     (22, 70, 16, 20, "quantized"),
-    (20, 40, 18, 12, "textured"),  # even k beyond the sliding instantiations: decided exactly
+    (20, 40, 18, 12, "textured"),  # even k > 17 on the sliding kernels
+    (20, 80, 34, 12, "textured"),  # even k beyond the sliding instantiations: decided exactly
 ]
 
 
@@ -250,8 +252,11 @@ BWD_CASES = [
     (16, 40, 25, 12, "smooth"),
     (20, 80, 31, 20, "textured"),
     (18, 100, 21, 64, "quantized"),  # with D = 64 n: the remainder kernel at k = 21
-    # generic fp64 backward (no fused instantiation): even k > 16, k > 31
+    # even k > 17 on the fused sweep (round 5)
     (17, 40, 18, 10, "textured"),
+    (20, 64, 30, 12, "smooth"),
+    # generic fp64 backward (no fused instantiation): k > 31
+    (17, 80, 34, 10, "textured"),
     (16, 44, 33, 10, "smooth"),
 ]
 
@@ -295,7 +300,7 @@ def test_backward_given_volume(gpu, case, layout):
     assert np.array_equal(gc, gc2.cpu().numpy()) and np.array_equal(gp, gp2.cpu().numpy())
 
 
-@pytest.mark.parametrize("case", [(20, 44, 33, 9, "textured"), (18, 40, 18, 10, "smooth")], ids=["k33", "k18"])
+@pytest.mark.parametrize("case", [(20, 44, 33, 9, "textured"), (18, 80, 34, 10, "smooth")], ids=["k33", "k34"])
 @pytest.mark.parametrize("layout", [FULL, WIN])
 def test_backward_generic_small_bands(gpu, case, layout, monkeypatch):
     """The generic fp64 backward's band loop (A / VA / BA recomputed per band of output rows, halo
