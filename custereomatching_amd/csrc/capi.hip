@@ -103,9 +103,10 @@ int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, vo
 // kept: the side stream starts after everything enqueued on s before the call, and s continues
 // after both halves.
 bool split_forward(const Geo& g) {
-    // CUSTMA_FWD_SPLIT=0 keeps the single-stream form (same-box A/B, scripts/kbench.py)
+    // opt-in (CUSTMA_FWD_SPLIT=1): measured slower than the single-stream form (same-process A/B/C,
+    // profiles/r05/a/ab_split.log: C3 1.030 vs 0.998 ms, C5 9.46 vs 9.35 ms)
     const char* e = getenv("CUSTMA_FWD_SPLIT");
-    if (e && e[0] == '0') return false;
+    if (!e || e[0] != '1') return false;
     if (g.layout != CUSTMA_LAYOUT_WINDOW || !disp_tile_ok(g)) return false;
     const int th = wave_grid(g).TH;
     return g.HV() >= 8 * th && (double)g.HV() * g.WO * g.DO * 4 >= 1e9;

@@ -780,8 +780,10 @@ hipError_t launch_disp_tile(const void* cam, const void* proj, int dtype, const 
 }
 
 bool fused_forward_ok(const Geo& g, const void* out) {
-    const char* e = getenv("CUSTMA_FWD_FUSED");  // 0: separate statistics pass (same-box A/B)
-    if (e && e[0] == '0') return false;
+    // opt-in (CUSTMA_FWD_FUSED=1): measured slower than the separate statistics pass + one sweep
+    // (same-process A/B/C, profiles/r05/a/ab_split.log: C3 1.030 vs 0.998 ms, C5 9.56 vs 9.35 ms)
+    const char* e = getenv("CUSTMA_FWD_FUSED");
+    if (!e || e[0] != '1') return false;
     if (g.layout != CUSTMA_LAYOUT_WINDOW || g.W % 32 != 0 || g.band_rows > 0 || g.k < 3) return false;
     const WaveGrid wg = wave_grid(g);
     const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0);

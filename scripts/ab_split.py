@@ -1,7 +1,7 @@
 """Same-process interleaved A/B/C of the forward's three forms at C3 and C5 window: the fused launch
-(statistics tiles inside the sweep's grid, the default), the split forward (CUSTMA_FWD_FUSED=0: two
-half-band sweeps on two streams) and the single stream (CUSTMA_FWD_FUSED=0 CUSTMA_FWD_SPLIT=0); both
-switches are read per call.  Forward op time from HIP events around the op; every form's volume must
+(CUSTMA_FWD_FUSED=1: statistics tiles inside the sweep's grid), the split forward (CUSTMA_FWD_SPLIT=1: two
+half-band sweeps on two streams) and the single stream (the default: the statistics pass, then one sweep);
+both switches are read per call.  Forward op time from HIP events around the op; every form's volume must
 equal the first one's bit for bit.  Usage: python scripts/ab_split.py [rounds]"""
 import json
 import os
@@ -15,8 +15,7 @@ import custereomatching_amd as cm  # noqa: E402
 from bench import EventTimer, synth_pair  # noqa: E402
 from kbench import CFGS, warm  # noqa: E402
 
-FORMS = {"fused": {}, "split": {"CUSTMA_FWD_FUSED": "0"},
-         "single": {"CUSTMA_FWD_FUSED": "0", "CUSTMA_FWD_SPLIT": "0"}}
+FORMS = {"fused": {"CUSTMA_FWD_FUSED": "1"}, "split": {"CUSTMA_FWD_SPLIT": "1"}, "single": {}}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 for name in ("c3_win", "c5_win"):
     c = CFGS[name]

@@ -279,6 +279,28 @@ def test_backward_both_images(gpu, case, layout):
     assert np.abs(gp - rp).max() <= tol_p, np.abs(gp - rp).max() / max(1.0, np.abs(rp).max())
 
 
+@pytest.mark.parametrize("case", [(18, 36, 4, 10, "textured"), (15, 30, 6, 8, "quantized"), (22, 120, 8, 64, "textured")],
+                         ids=["18x36_k4", "15x30_k6", "22x120_k8_D64"])
+def test_backward_even_k_window_repeated(gpu, case):
+    """The round-4 suite failed once on the window k = 4 backward (camera gradient 2.1e-4 relative) and the
+    failure did not reproduce at round-5 HEAD: the even-k window backward, recompute path, 20 times on the
+    same inputs -- every call bit-identical and within the bar (an intermittent race would show here)."""
+    H, W, k, D, kind = case
+    cam, proj = make_pair(H, W, max(D, 1), seed=31, kind=kind)
+    g = _rand_grad(O.volume_shape(H, W, O.WINDOW, D), 7)
+    rc, rp = O.backward_f64(g, cam, proj, k, layout=O.WINDOW, D=D)
+    c, p, gd = _dev(cam, gpu), _dev(proj, gpu), _dev(g, gpu)
+    first = None
+    for _ in range(20):
+        gc, gp = cm.cost_volume_backward(gd, c, p, k, WIN, D, camera_grad=True, projector_grad=True)
+        if first is None:
+            first = (gc, gp)
+            assert np.abs(gc.cpu().numpy() - rc).max() <= 1e-5 * max(1.0, np.abs(rc).max())
+            assert np.abs(gp.cpu().numpy() - rp).max() <= 1e-5 * max(1.0, np.abs(rp).max())
+        else:
+            assert torch.equal(gc, first[0]) and torch.equal(gp, first[1])
+
+
 @pytest.mark.parametrize("case", BWD_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_D{c[3]}_{c[4]}" for c in BWD_CASES])
 @pytest.mark.parametrize("layout", [FULL, WIN])
 def test_backward_given_volume(gpu, case, layout):
@@ -583,7 +605,7 @@ def _split_inputs(gpu):
 def test_split_forward_matches_half_bands(gpu, monkeypatch):
     """The two-stream forward equals the same rows computed as two separate band calls (each below the
     split size), bit for bit, and stays within the fast tolerance of the exact volume."""
-    monkeypatch.setenv("CUSTMA_FWD_FUSED", "0")
+    monkeypatch.setenv("CUSTMA_FWD_SPLIT", "1")  # opt-in (slower than the single stream, DESIGN §3.1)
     c, p, H, D, k = _split_inputs(gpu)
     full = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
     torch.cuda.synchronize()
@@ -604,7 +626,7 @@ def test_split_forward_matches_half_bands(gpu, monkeypatch):
 def test_split_forward_graph_capture(gpu, monkeypatch):
     """Under stream capture the forward records its single-stream form (capi.hip: the side-stream
     split is for eager calls): a replay on new inputs equals the eager (split) forward bit for bit."""
-    monkeypatch.setenv("CUSTMA_FWD_FUSED", "0")
+    monkeypatch.setenv("CUSTMA_FWD_SPLIT", "1")
     c, p, H, D, k = _split_inputs(gpu)
     out = torch.empty(H, c.shape[1] - D, D + 1, device=gpu)
     side = torch.cuda.Stream(gpu)
@@ -639,20 +661,18 @@ FUSED_CASES = [
 
 @pytest.mark.parametrize("case", FUSED_CASES, ids=[f"{c[0]}x{c[1]}_D{c[2]}_k{c[3]}" for c in FUSED_CASES])
 def test_fused_forward_matches_separate_statistics(gpu, monkeypatch, case):
-    """The fused launch writes the volume bit for bit as the separate statistics pass + sweep do, also
-    when replayed from a hipGraph; sampled rows stay within the fast tolerance of the exact volume."""
+    """The fused launch (CUSTMA_FWD_FUSED=1) writes the volume bit for bit as the separate statistics
+    pass + sweep do, also when replayed from a hipGraph; sampled rows stay within the fast tolerance
+    of the exact volume."""
     H, W, D, k, dt = case
     cam, proj = make_pair(H, W, D, seed=71)
     c, p = _dev(cam, gpu, dt), _dev(proj, gpu, dt)
+    sep = cm.cost_volume_forward(c, p, D, k, WIN, "fast")  # default: separate statistics pass, one sweep
+    monkeypatch.setenv("CUSTMA_FWD_FUSED", "1")  # opt-in (measured slower, DESIGN §3.1)
     fused = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
-    monkeypatch.setenv("CUSTMA_FWD_FUSED", "0")
-    monkeypatch.setenv("CUSTMA_FWD_SPLIT", "0")
-    sep = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
     torch.cuda.synchronize()
     assert torch.equal(fused, sep)
     del sep
-    monkeypatch.delenv("CUSTMA_FWD_FUSED")
-    monkeypatch.delenv("CUSTMA_FWD_SPLIT")
     out = torch.empty_like(fused)
     s = torch.cuda.Stream(gpu)
     s.wait_stream(torch.cuda.current_stream(gpu))
