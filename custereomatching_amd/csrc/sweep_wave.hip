@@ -520,11 +520,17 @@ constexpr int kWaveLds = (3 * kRowP + 64) * 8 + kRowP * 4;  // rowE, rowL, sM, s
 // waits only for tiles of LOWER hardware index, so the grid cannot deadlock whatever the placement
 // (blocks start in index order); the poll is bounded, never a hang.
 constexpr int kFusedMinK = 3;
+// CUSTMA_FWD_FUSED=2: the sweep tiles take one agent-scope acquire after their poll and read the
+// statistics with plain loads (=1: `sc1` loads, no acquire)
+inline bool fused_acquire() {
+    const char* e = getenv("CUSTMA_FWD_FUSED");
+    return e && e[0] == '2';
+}
 struct FusedGrid {
     int nBand, nTile, nSC, P, perX, len;  // P = 2 nSC statistics tiles per band; perX bands per XCD
 };
 
-template <int K, typename T, bool X4, int AMX = 0, bool CPL = false, bool FUSED = false>
+template <int K, typename T, bool X4, int AMX = 0, bool CPL = false, bool FUSED = false, bool FUSED_ACQ = false>
 __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __restrict__ cam,
                                                                  const T* __restrict__ proj, Geo g, Stats sc,
                                                                  Stats sp, float* __restrict__ out, WaveGrid wg,
@@ -567,10 +573,16 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
             if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + sb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
-        if (threadIdx.x == 0) {  // wait for the band's statistics (bounded: ~0.5 s, then go on)
+        if (threadIdx.x == 0) {  // wait for the band's statistics (bounded: ~0.2 s, then go on)
             for (int it = 0; it < (1 << 20); ++it) {
                 if (__hip_atomic_load(cnt + band, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= fg.P) break;
                 __builtin_amdgcn_s_sleep(8);
+            }
+            // FUSED_ACQ: one agent-scope acquire (this CU's L1 invalidated), then the statistics are read
+            // with plain loads; else every statistics load is an `sc1` load
+            if constexpr (FUSED_ACQ) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
         __syncthreads();
@@ -595,13 +607,13 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
     constexpr int kTP = X4 ? kTileP : 2;  // deeper pipelines only with the 16-byte stores (vmcnt range)
     if (!wg.rem)
-        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                          rowL, sM, sQ, sR, stage, part, camL);
     else if (w == wg.nChunk - 1)
-        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                         rowL, sM, sQ, sR, stage, part, camL);
     else
-        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                          rowL, sM, sQ, sR, stage, part, camL);
 }
 
@@ -678,17 +690,22 @@ hipError_t launch_fused(const T* cam, const T* proj, const Geo& g, Stats sc, Sta
     if (e != hipSuccess) return e;
     const dim3 grid((unsigned)(8 * (int64_t)fg.len)), blk(64 * wg.nChunk);
     prof_begin(PROF_FWD, s);
+    auto go = [&](auto cpl_, auto acq_) -> hipError_t {
+        constexpr bool CPLV = decltype(cpl_)::value, ACQ = decltype(acq_)::value;
+        hipError_t r = allow_lds(k_fwd_tile<K, T, true, 0, CPLV, true, ACQ>, lds);
+        if (r != hipSuccess) return r;
+        hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, CPLV, true, ACQ>), grid, blk, lds, s, cam, proj, g, sc, sp, out,
+                           wg, DispPartial{}, cnt, fg);
+        return hipSuccess;
+    };
+    const bool acq = fused_acquire();
     if (cpl) {
-        if constexpr (sizeof(T) == 2) {
-            if ((e = allow_lds(k_fwd_tile<K, T, true, 0, true, true>, lds)) != hipSuccess) return e;
-            hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, true, true>), grid, blk, lds, s, cam, proj, g, sc, sp, out, wg,
-                               DispPartial{}, cnt, fg);
-        }
+        if constexpr (sizeof(T) == 2)
+            e = acq ? go(std::true_type{}, std::true_type{}) : go(std::true_type{}, std::false_type{});
     } else {
-        if ((e = allow_lds(k_fwd_tile<K, T, true, 0, false, true>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, false, true>), grid, blk, lds, s, cam, proj, g, sc, sp, out, wg,
-                           DispPartial{}, cnt, fg);
+        e = acq ? go(std::false_type{}, std::true_type{}) : go(std::false_type{}, std::false_type{});
     }
+    if (e != hipSuccess) return e;
     prof_end(PROF_FWD, s);
     return hipGetLastError();
     }
@@ -783,7 +800,7 @@ bool fused_forward_ok(const Geo& g, const void* out) {
     // opt-in (CUSTMA_FWD_FUSED=1): measured slower than the separate statistics pass + one sweep
     // (same-process A/B/C, profiles/r05/a/ab_split.log: C3 1.030 vs 0.998 ms, C5 9.56 vs 9.35 ms)
     const char* e = getenv("CUSTMA_FWD_FUSED");
-    if (!e || e[0] != '1') return false;
+    if (!e || (e[0] != '1' && e[0] != '2')) return false;
     if (g.layout != CUSTMA_LAYOUT_WINDOW || g.W % 32 != 0 || g.band_rows > 0 || g.k < 3) return false;
     const WaveGrid wg = wave_grid(g);
     const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0);

@@ -659,8 +659,9 @@ FUSED_CASES = [
 ]
 
 
+@pytest.mark.parametrize("form", ["1", "2"], ids=["sc1", "acquire"])
 @pytest.mark.parametrize("case", FUSED_CASES, ids=[f"{c[0]}x{c[1]}_D{c[2]}_k{c[3]}" for c in FUSED_CASES])
-def test_fused_forward_matches_separate_statistics(gpu, monkeypatch, case):
+def test_fused_forward_matches_separate_statistics(gpu, monkeypatch, case, form):
     """The fused launch (CUSTMA_FWD_FUSED=1) writes the volume bit for bit as the separate statistics
     pass + sweep do, also when replayed from a hipGraph; sampled rows stay within the fast tolerance
     of the exact volume."""
@@ -668,7 +669,7 @@ def test_fused_forward_matches_separate_statistics(gpu, monkeypatch, case):
     cam, proj = make_pair(H, W, D, seed=71)
     c, p = _dev(cam, gpu, dt), _dev(proj, gpu, dt)
     sep = cm.cost_volume_forward(c, p, D, k, WIN, "fast")  # default: separate statistics pass, one sweep
-    monkeypatch.setenv("CUSTMA_FWD_FUSED", "1")  # opt-in (measured slower)
+    monkeypatch.setenv("CUSTMA_FWD_FUSED", form)  # opt-in (measured slower)
     fused = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
     torch.cuda.synchronize()
     assert torch.equal(fused, sep)
