@@ -109,7 +109,6 @@ struct SweepGrid {
     int TH;      // rows per band
     int NL;      // diagonal lanes per workgroup (compute waves x 64)
     int S;       // chunk stride in volume columns (== NL unless chunks own aligned columns)
-    int x4 = 1;  // k_sweep_fwd may use its 16-byte store form (CUSTMA_FULL_X4=0 turns it off: A/B)
 };
 
 struct DispPartial {

@@ -311,7 +311,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     // ...: lane j the 4 owned columns cb + 4 j .. cb + 4 j + 3 (read from the staged row with 4 LDS reads,
     // one dwordx4 store) -- 4 (5 waves: <= 8) store instructions per lane and step instead of 16 dword ones.
     // (cb, ce) of a row are wave-uniform, so the range check is one compare per store.
-    const bool x4 = sg.x4 && ((g.WO * g.DO) & 15) == 0 && (g.DO & 15) == 0 && ((uintptr_t)out & 15) == 0;
+    const bool x4 = ((g.WO * g.DO) & 15) == 0 && (g.DO & 15) == 0 && ((uintptr_t)out & 15) == 0;
     const int nW = NL >> 6, wv = tid >> 6, lane = tid & 63;
     auto store_tile4 = [&](int64_t h, int b) {
         const auto rOut = make_rsrc(out + ((h - g.h_lo) * g.WO + u0) * g.DO, 0x7FFFFFF0u);
@@ -450,8 +450,7 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
                     DispPartial* part, hipStream_t s) {
     // (per-lane 256-byte stores straight from registers, one chunk of all D+1 diagonals of a window,
     // measured slower: 2.56 vs 2.34 ms at 2048^2, D = 256, k = 11)
-    SweepGrid sg = sweep_grid(g, /*owned=*/part == nullptr);
-    if (const char* e = getenv("CUSTMA_FULL_X4")) sg.x4 = e[0] != '0';
+    const SweepGrid sg = sweep_grid(g, /*owned=*/part == nullptr);
     constexpr int NX = TW + K - 1;
     constexpr int NL_MAX = 320, OP = 64 * ((NX + NL_MAX - 1 + 63) / 64), SP = 64 * ((TW + NL_MAX - 1 + 63) / 64);
     const int NL = sg.NL;
