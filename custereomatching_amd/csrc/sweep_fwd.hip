@@ -306,38 +306,11 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         for (int m = 0; m < TWT; ++m) st_vol(v[m], rOut, voff[m]);
     };
 
-    // 16-byte form (round 5): when every owned range starts on a 16-float boundary (the sector phase is
-    // fixed and zero: DO % 16 == 0) and the volume is 16-byte aligned, wave w stores tile rows w, w + nW,
-    // ...: lane j the 4 owned columns cb + 4 j .. cb + 4 j + 3 (read from the staged row with 4 LDS reads,
-    // one dwordx4 store) -- 4 (5 waves: <= 8) store instructions per lane and step instead of 16 dword ones.
-    // (cb, ce) of a row are wave-uniform, so the range check is one compare per store.
-    const bool x4 = ((g.WO * g.DO) & 15) == 0 && (g.DO & 15) == 0 && ((uintptr_t)out & 15) == 0;
-    const int nW = NL >> 6, wv = tid >> 6, lane = tid & 63;
-    auto store_tile4 = [&](int64_t h, int b) {
-        const auto rOut = make_rsrc(out + ((h - g.h_lo) * g.WO + u0) * g.DO, 0x7FFFFFF0u);
-        const float* tile = stg + b * 16 * NL;
-        for (int m = wv; m < TWT; m += nW) {
-            if (u0 + m >= g.WO) break;
-            const int cb = bound(chunk, 0), ce = bound(chunk + 1, 0);
-            for (int j = lane; 4 * j < ce - cb; j += 64) {
-                const int c = cb + 4 * j;
-                // staging slot of column c in row m: m NL + c - d0 - (u0 + m) (full) / m NL + c - d0 (window)
-                const float* src = tile + m * NL + c + stgB + (window ? 0 : -m);
-                const i32x4 v = {__builtin_bit_cast(int, src[0]), __builtin_bit_cast(int, src[1]),
-                                 __builtin_bit_cast(int, src[2]), __builtin_bit_cast(int, src[3])};
-                __builtin_amdgcn_raw_buffer_store_b128(v, rOut, (uint32_t)((m * DO + c) * 4), 0u, kStoreAux);
-            }
-        }
-    };
-
     __syncthreads();  // the loader's first stage
     for (int64_t h = hs; h < h1; ++h) {
         const int buf = (int)((h - hs) & 1);
         if constexpr (!ARGMAX) {
-            if (h > h0) {
-                if (x4) store_tile4(h - 1, buf ^ 1);
-                else store_tile(h - 1, buf ^ 1);
-            }
+            if (h > h0) store_tile(h - 1, buf ^ 1);
         }
         update(buf);
         if (h >= h0) {
@@ -437,10 +410,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
         __syncthreads();
     }
     if constexpr (!ARGMAX) {
-        if (h1 > h0) {
-            if (x4) store_tile4(h1 - 1, (int)((h1 - 1 - hs) & 1));
-            else store_tile(h1 - 1, (int)((h1 - 1 - hs) & 1));
-        }
+        if (h1 > h0) store_tile(h1 - 1, (int)((h1 - 1 - hs) & 1));
         __syncthreads();
     }
 }
