@@ -512,19 +512,24 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         const float w0r = u0 + u1, w1r = u2 + u3, w2r = u4 + u5;
         cbuf[slot][qlane] = reduce_tail3(w0r, w1r, w2r, lane);
     };
-    auto step = [&](Ld& cur, Ld& nxt, int w, int s, bool flushed) {
+    // fl_c: BDP == 1 -- std::true_type at a block's first step (after the previous block's flush, or
+    // after the prologue's wait), std::false_type elsewhere, so every wait is fixed at compile time
+    // and vmcnt_check.py can prove it on the emitted code; BDP == 2 -- a runtime bool (flushed)
+    auto step = [&](Ld& cur, Ld& nxt, int w, int s, auto fl_c) {
         if constexpr (BDP == 2) {
+            const bool flushed = fl_c;
             // a column block issued at s = 0 (after the flush's stores) feeds step 1
             if (!flushed || s >= 1) asm_vmcnt<NL>();
             else if (s == 1) asm_vmcnt<NL + SF>();
-        } else {
+        } else if constexpr (std::is_same<decltype(fl_c), std::true_type>::value) {
             // the step's loads, not the flush's SF stores issued after them: a store's completion
             // is not needed here, and on gfx950 `s_waitcnt vmcnt(N)` counts loads, stores, atomics
             // and LDS-DMA together in issue order, so vmcnt(SF) waits for every load issued before
             // those SF stores (MI355X_MICROARCH.md, the vmcnt paragraph after the cycle constants;
             // LLVM's own waitcnt pass does not assume this ordering, hence the hand-counted wait)
-            if (flushed && s == 0) asm_vmcnt<SF>();
-            else asm_vmcnt<0>();
+            asm_vmcnt<SF>();
+        } else {
+            asm_vmcnt<0>();
         }
         tie(cur);
         if (w > w0) {  // move the columns down one lane; lane 63 takes column w + 63 (+ offset)
@@ -621,10 +626,19 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     load_cam(w0);  // CAML: the first block (written to LDS at step w0)
     issue(w0, L[0], std::true_type{});
     if constexpr (BDP == 2) issue(w0 + 1, L[1], std::true_type{});
-    for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
-        const int nsteps = min(FBC, wend - wfirst);  // FBC = a multiple of BDP + 1: blocks start on L[0]
-        const bool fl = wfirst > w0;
-        if constexpr (BDP == 2) {
+    // The prologue's loads land before the loop: the compiler joins the prologue to the loop with
+    // register copies where it assigns the loop's registers differently (it takes an asm load's
+    // destination as written at issue), and a copy of a register whose load is still in flight reads
+    // what the previous wave on the SIMD left there.  (k = 2..4 did: the window k = 4 backward was
+    // wrong on cold caches -- the first call of a process, or after another large kernel.)
+    asm_vmcnt<0>();
+#pragma unroll
+    for (int i = 0; i <= BDP; ++i) tie(L[i]);
+    tie_cols();
+    if constexpr (BDP == 2) {
+        for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
+            const int nsteps = min(FBC, wend - wfirst);  // FBC = a multiple of BDP + 1: blocks start on L[0]
+            const bool fl = wfirst > w0;
             for (int s = 0; s < nsteps; s += 3) {
                 step(L[0], L[2], wfirst + s, s, fl);
                 if (s + 1 >= nsteps) break;
@@ -632,15 +646,42 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
                 if (s + 2 >= nsteps) break;
                 step(L[2], L[1], wfirst + s + 2, s + 2, fl);
             }
-        } else {
-            for (int s = 0; s < nsteps; s += 2) {
-                step(L[0], L[1], wfirst + s, s, fl);
-                if (s + 1 >= nsteps) break;
-                step(L[1], L[0], wfirst + s + 1, s + 1, fl);
-            }
+            reduce_to(nsteps - 1);
+            flush(wfirst, nsteps);
         }
-        reduce_to(nsteps - 1);
-        flush(wfirst, nsteps);
+    } else {
+        // Full blocks (FBC steps, FBC even: a block starts and ends on L[0]), then the last, shorter
+        // one.  No exit of the full-block loop depends on a step count, so the compiler's control-flow
+        // graph has no path from a block that ended on an odd step into the next block (on such a path
+        // it may take the pending L[1] loads as dead and reuse their registers, vmcnt_check.py).
+        static_assert(FBC % 2 == 0, "a full block ends on L[0]");
+        int wfirst = w0;
+        for (; wfirst + FBC <= wend; wfirst += FBC) {
+            step(L[0], L[1], wfirst, 0, std::true_type{});
+            for (int s = 1; s < FBC - 1; s += 2) {
+                step(L[1], L[0], wfirst + s, s, std::false_type{});
+                step(L[0], L[1], wfirst + s + 1, s + 1, std::false_type{});
+            }
+            step(L[1], L[0], wfirst + FBC - 1, FBC - 1, std::false_type{});
+            reduce_to(FBC - 1);
+            flush(wfirst, FBC);
+        }
+        // (the last step's loads have landed where the two paths below join: the compiler joins them
+        // with register copies too -- of loads past the segment's end, dead, but kept provable)
+        asm_vmcnt<0>();
+        tie(L[0]);
+        tie_cols();
+        if (wfirst < wend) {
+            const int nsteps = wend - wfirst;
+            step(L[0], L[1], wfirst, 0, std::true_type{});
+            for (int s = 1; s < nsteps; s += 2) {
+                step(L[1], L[0], wfirst + s, s, std::false_type{});
+                if (s + 1 >= nsteps) break;
+                step(L[0], L[1], wfirst + s + 1, s + 1, std::false_type{});
+            }
+            reduce_to(nsteps - 1);
+            flush(wfirst, nsteps);
+        }
     }
     // The last steps' prefetches are still in flight: keep their registers live (the compiler
     // would otherwise reuse them in the last flush) until they have landed.

@@ -198,18 +198,24 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     // issues, so a peeled prologue with another register assignment would be joined to the
     // loop by register copies -- reads of registers whose loads are still in flight.
     Stage st[P];
-    auto compute = [&](Stage& p, int64_t t) {
+    // stores per step (every thread issues exactly ST: the hand-counted waits rely on it)
+    constexpr int ST = AMX > 0 ? (SOFT ? 5 : 3) * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);
+    static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
+    // out_c: std::true_type for an output step (t >= h0: stores), std::false_type for a warm-up step
+    // (P == 2: both fixed at compile time, so the waits are too); a runtime bool with P == 3
+    auto compute = [&](Stage& p, int64_t t, auto out_c) {
+        const bool out = out_c;
         // loads(t) were issued at the end of step t-P; after them, for each step s in
         // t-P+1 .. t-1: its stores (from step h0 on) and loads(s+P)
-        constexpr int ST = AMX > 0 ? (SOFT ? 5 : 3) * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);
-        static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
         if constexpr (P == 3) {
             if (t - 2 >= h0) asm_vmcnt<2 * (kLoads + ST)>();
             else if (t - 1 >= h0) asm_vmcnt<2 * kLoads + ST>();
             else asm_vmcnt<2 * kLoads>();
+        } else if constexpr (std::is_same<decltype(out_c), std::true_type>::value) {
+            // the previous step stored (or, for t = h0, the null stores between the phases stand in)
+            asm_vmcnt<kLoads + ST>();
         } else {
-            if (t - 1 >= h0) asm_vmcnt<kLoads + ST>();
-            else asm_vmcnt<kLoads>();
+            asm_vmcnt<kLoads>();
         }
         tie(p);
         rowE[l] = raw_to_f64<T>(p.pe0);
@@ -290,7 +296,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             colR = __builtin_fma(cRe, *(const lds_vd*)(rowE + 64 + l), colR);
             colR = __builtin_fma(cRl, *(const lds_vd*)(rowL + 64 + l), colR);
         }
-        if (t >= h0) {
+        if (out) {
             const auto rOut = make_rsrc(orow, tile_bytes);
             orow += ostep;
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
@@ -315,6 +321,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             // every lane of the chunk valid (all but a partial last chunk): unmasked stage writes,
             // no per-output exec branch
             const bool allv = d0 + 63 <= g.D;
+            // FULL_EDGE: the column base opaque per step, so that the per-row store offsets below are
+            // not hoisted out of the output loop (16 VGPRs held across it: 141 -> 169 VGPRs)
+            int64_t a0S = a0;
+            if constexpr (FULL_EDGE) asm volatile("" : "+v"(a0S));
             auto outputs = [&](auto masked_c) {
             constexpr bool MASKED = decltype(masked_c)::value;
             Unroll<0, TW>::run([&](auto mc) {
@@ -333,7 +343,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
                 uint32_t vo = vOut, so = (uint32_t)(m * sstep);
                 if constexpr (FULL_EDGE) {  // per-row mask; the whole offset in voffset
-                    vo = ((uint64_t)(a0 + m) < (uint64_t)g.W) ? (uint32_t)((a0 + m + m * DO) * 4) : OOB;
+                    vo = ((uint64_t)(a0S + m) < (uint64_t)g.W) ? (uint32_t)((a0S + m + m * DO) * 4) : OOB;
                     so = 0;
                 }
                 if constexpr (STAGED) {
@@ -367,7 +377,12 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 // every wave's part of the 16 rows is in LDS: store the block (256 contiguous
                 // bytes per wave instruction, the whole workgroup's instruction contiguous)
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                const int NT = (int)blockDim.x, tid = (int)threadIdx.x;
+                const int NT = (int)blockDim.x;
+                // opaque per step: the block's store offsets are recomputed at each step instead of
+                // hoisted out of the output loop, where they would hold SS VGPRs across it (141 -> 166-171
+                // VGPRs, two waves per SIMD instead of three)
+                int tid = (int)threadIdx.x;
+                asm volatile("" : "+v"(tid));
                 const int total = (int)(nrow * DO);
                 if constexpr (AMX > 0) {
                     const int wv = tid >> 6, nw = NT >> 6, sub = l & 15;
@@ -453,25 +468,64 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             }
         }
     };
-    auto step = [&](auto kc, int64_t t) {
+    // comp: compute the step (false: the first P steps, which only issue loads); P == 2 passes
+    // compile-time constants throughout, so no step has a runtime test around its compute
+    auto step = [&](auto kc, int64_t t, auto out_c, auto comp) {
         Stage& p = st[decltype(kc)::value];
-        if (t >= hs) compute(p, t);
+        if (comp) compute(p, t, out_c);
         // past the band's end: harmless (rows out of range read zeros)
         load_step(t + P, p);
     };
-    int64_t t_first = hs - P;  // opaque: the warm-up iterations must not be peeled
-    asm volatile("" : "+s"(t_first));
-    for (int64_t t = t_first;; t += P) {
-        step(std::integral_constant<int, 0>{}, t);
-        if (t + 1 >= h1) break;
-        step(std::integral_constant<int, 1>{}, t + 1);
-        if (t + 2 >= h1) break;
-        if constexpr (P == 3) {
-            step(std::integral_constant<int, 2 % P>{}, t + 2);
+    const std::true_type yes{};
+    const std::false_type no{};
+    if constexpr (P == 2) {
+        // Three phases, every wait fixed at compile time, so that vmcnt_check.py can prove them on the
+        // emitted code (a runtime choice between two waits, a runtime test around a step's compute, or a
+        // `break` after each step gives paths the hardware never takes, on which the proof fails):
+        //   t = hs - 2, hs - 1:  loads only;
+        //   t = hs .. h0 - 1:    the K - 1 warm-up steps, no stores;
+        //   t = h0 .. h1 - 1:    ST stores per step -- pairs with the loop's only exit at its test, then
+        //                        an odd last step; ST null stores before it stand in for the stores of
+        //                        the step before t = h0.
+        // The stage buffers alternate throughout: the output phase starts on st[(K - 1) % 2].
+        constexpr int A = (K - 1) % 2;
+        int64_t t = hs - 2;
+        asm volatile("" : "+s"(t));  // (opaque: the load-only steps stay one issue each)
+        step(std::integral_constant<int, 0>{}, t, no, no);
+        step(std::integral_constant<int, 1>{}, t + 1, no, no);
+        t += 2;
+#pragma unroll 1
+        for (int i = 0; i < (K - 1) / 2; ++i, t += 2) {
+            step(std::integral_constant<int, 0>{}, t, no, yes);
+            step(std::integral_constant<int, 1>{}, t + 1, no, yes);
+        }
+        if constexpr (A == 1) {
+            step(std::integral_constant<int, 0>{}, t, no, yes);
+            ++t;
+        }
+        asm_null_stores<ST>(dCam);
+        for (; t + 1 < h1; t += 2) {
+            step(std::integral_constant<int, A>{}, t, yes, yes);
+            step(std::integral_constant<int, 1 - A>{}, t + 1, yes, yes);
+        }
+        if (t < h1) step(std::integral_constant<int, A>{}, t, yes, yes);
+    } else {
+        int64_t t_first = hs - P;  // opaque: the warm-up iterations must not be peeled
+        asm volatile("" : "+s"(t_first));
+        for (int64_t t = t_first;; t += P) {
+            step(std::integral_constant<int, 0>{}, t, t >= h0, t >= hs);
+            if (t + 1 >= h1) break;
+            step(std::integral_constant<int, 1>{}, t + 1, t + 1 >= h0, t + 1 >= hs);
+            if (t + 2 >= h1) break;
+            step(std::integral_constant<int, 2 % P>{}, t + 2, t + 2 >= h0, t + 2 >= hs);
             if (t + 3 >= h1) break;
         }
     }
     asm_vmcnt<0>();  // every wave drains its own loads before it ends
+    // The last steps' loads (rows past the band) are dead, but their registers must not be reused
+    // before they land -- a late load would overwrite the new value: keep them live until here.
+#pragma unroll
+    for (int i = 0; i < P; ++i) tie(st[i]);
 }
 
 template <int K, typename T>
