@@ -301,6 +301,56 @@ def test_backward_even_k_window_repeated(gpu, case):
             assert torch.equal(gc, first[0]) and torch.equal(gp, first[1])
 
 
+_COLD = {}
+
+
+def _cold_caches(gpu):
+    """A large exact forward (256 x 2048 fp16, k = 19, D = 256: 0.47 GB written) between the calls: the next
+    kernel starts with cold TLB and caches, and its waves inherit registers and LDS the exact kernel left --
+    the state in which the round-4/5 window k = 4 backward read registers whose loads were still in flight
+    (DESIGN.md §3.6)."""
+    if "pair" not in _COLD:
+        from bench import synth_pair
+        _COLD["pair"] = synth_pair(256, 2048, 256, 5, str(gpu), torch.float16)
+    c3, p3 = _COLD["pair"]
+    v = cm.cost_volume_forward(c3, p3, 256, 19, WIN, "exact")
+    torch.cuda.synchronize()
+    del v
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 5, 6, 11])
+@pytest.mark.parametrize("layout", [FULL, WIN])
+def test_ops_after_a_large_kernel(gpu, k, layout):
+    """Every op right after a large kernel (cold caches, foreign register / LDS contents) equals the same op
+    run warm, bit for bit: forward, backward with and without the volume, disparity."""
+    H, W, D = 18, 36, 10
+    cam, proj = make_pair(H, W, D, seed=31, kind="textured")
+    lay, Dl = _layout_args(layout, D)
+    g = _rand_grad(O.volume_shape(H, W, lay, Dl), 7)
+    c, p, gd = _dev(cam, gpu), _dev(proj, gpu), _dev(g, gpu)
+    def tensors(x):
+        return [x] if torch.is_tensor(x) else [y for y in x if torch.is_tensor(y)]
+
+    ops = {
+        "forward": lambda: cm.cost_volume_forward(c, p, Dl, k, layout, "fast"),
+        "backward(volume)": lambda: cm.cost_volume_backward(gd, c, p, k, layout, Dl, camera_grad=True,
+                                                            projector_grad=True, cost_volume=warm_vol),
+        "backward(recompute)": lambda: cm.cost_volume_backward(gd, c, p, k, layout, Dl, camera_grad=True,
+                                                               projector_grad=True),
+    }
+    if layout == WIN:
+        ops["disparity"] = lambda: cm.stereo_disparity(c, p, Dl, k, layout)
+    warm_vol = cm.cost_volume_forward(c, p, Dl, k, layout, "fast")
+    for name, op in ops.items():
+        op()
+        ref = [x.clone() for x in tensors(op())]
+        _cold_caches(gpu)
+        got = tensors(op())
+        assert len(got) == len(ref) > 0
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b), f"{name}: differs after a large kernel"
+
+
 @pytest.mark.parametrize("case", BWD_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_D{c[3]}_{c[4]}" for c in BWD_CASES])
 @pytest.mark.parametrize("layout", [FULL, WIN])
 def test_backward_given_volume(gpu, case, layout):
