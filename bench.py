@@ -410,8 +410,8 @@ def main():
     _lib.profile_enable(False)
     per_rank = None
     if distributed:
-        # per rank: sweep kernel times (HIP events; the forward's interior + edge launches are
-        # separate launches) and the exchange times the op's stream waited for (rowband timing)
+        # per rank: sweep kernel times (HIP events; one forward sweep launch per step, three with
+        # CUSTMA_ROWBAND_OVERLAP=1) and the exchange times the op's stream waited for (rowband timing)
         mine = {"rank": rank, "rows": int(cam.shape[0]), "fwd_sweep_launch_ms": round(fwd_kms, 4),
                 "fwd_sweep_launches_per_step": round(n_fk / max(1, args.steps), 2),
                 "bwd_sweep_launch_ms": round(bwd_kms, 4), "step_ms_local": round(elapsed / args.steps * 1e3, 4)}
@@ -452,8 +452,9 @@ def main():
     bwd_bytes = nvox_rank * 4 + img + 2 * cam.numel() * 4
     bwd_design = bwd_bytes + nvox_rank * 4
     fwd_name = fwd_kernel_name(layout, W, D)
-    # The forward's bytes are per step; at N > 1 it runs as an interior launch + two edge launches
-    # (rowband), and a large band's sweep may run as two half-band launches that overlap in time
+    # The forward's bytes are per step; at N > 1 with CUSTMA_ROWBAND_OVERLAP=1 it runs as an interior
+    # launch + two edge launches (rowband), and a large band's sweep may run as two half-band launches
+    # that overlap in time
     # (DESIGN.md §3.1).  So its rate is taken over the forward op's whole span per step (events on the
     # op's stream before and after the op: statistics pass included, overlapped launches counted once),
     # never over a sum of launch times.

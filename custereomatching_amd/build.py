@@ -66,6 +66,11 @@ def _check_hazards(unit, extra, libdir):
     if r.returncode != 0:
         os.remove(_obj(unit, libdir))
         raise RuntimeError(f"wait-state hazards in {name} ({src}):\n{r.stdout}")
+    # and no instruction touches a register whose (hand-waited) load is still in flight
+    r = subprocess.run([sys.executable, os.path.join(HERE, "vmcnt_check.py"), listing], capture_output=True, text=True)
+    if r.returncode != 0:
+        os.remove(_obj(unit, libdir))
+        raise RuntimeError(f"registers read with their load in flight in {name} ({src}):\n{r.stdout}")
     with open(listing) as f:
         scratch = scratch_lines(f.read())
     if scratch:

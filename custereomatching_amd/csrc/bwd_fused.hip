@@ -512,19 +512,24 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         const float w0r = u0 + u1, w1r = u2 + u3, w2r = u4 + u5;
         cbuf[slot][qlane] = reduce_tail3(w0r, w1r, w2r, lane);
     };
-    auto step = [&](Ld& cur, Ld& nxt, int w, int s, bool flushed) {
+    // fl_c: BDP == 1 -- std::true_type at a block's first step (after the previous block's flush, or
+    // after the prologue's wait), std::false_type elsewhere, so every wait is fixed at compile time
+    // and vmcnt_check.py can prove it on the emitted code; BDP == 2 -- a runtime bool (flushed)
+    auto step = [&](Ld& cur, Ld& nxt, int w, int s, auto fl_c) {
         if constexpr (BDP == 2) {
+            const bool flushed = fl_c;
             // a column block issued at s = 0 (after the flush's stores) feeds step 1
             if (!flushed || s >= 1) asm_vmcnt<NL>();
             else if (s == 1) asm_vmcnt<NL + SF>();
-        } else {
+        } else if constexpr (std::is_same<decltype(fl_c), std::true_type>::value) {
             // the step's loads, not the flush's SF stores issued after them: a store's completion
             // is not needed here, and on gfx950 `s_waitcnt vmcnt(N)` counts loads, stores, atomics
             // and LDS-DMA together in issue order, so vmcnt(SF) waits for every load issued before
             // those SF stores (MI355X_MICROARCH.md, the vmcnt paragraph after the cycle constants;
             // LLVM's own waitcnt pass does not assume this ordering, hence the hand-counted wait)
-            if (flushed && s == 0) asm_vmcnt<SF>();
-            else asm_vmcnt<0>();
+            asm_vmcnt<SF>();
+        } else {
+            asm_vmcnt<0>();
         }
         tie(cur);
         if (w > w0) {  // move the columns down one lane; lane 63 takes column w + 63 (+ offset)
@@ -621,10 +626,19 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
     load_cam(w0);  // CAML: the first block (written to LDS at step w0)
     issue(w0, L[0], std::true_type{});
     if constexpr (BDP == 2) issue(w0 + 1, L[1], std::true_type{});
-    for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
-        const int nsteps = min(FBC, wend - wfirst);  // FBC = a multiple of BDP + 1: blocks start on L[0]
-        const bool fl = wfirst > w0;
-        if constexpr (BDP == 2) {
+    // The prologue's loads land before the loop: the compiler joins the prologue to the loop with
+    // register copies where it assigns the loop's registers differently (it takes an asm load's
+    // destination as written at issue), and a copy of a register whose load is still in flight reads
+    // what the previous wave on the SIMD left there.  (k = 2..4 did: the window k = 4 backward was
+    // wrong on cold caches -- the first call of a process, or after another large kernel.)
+    asm_vmcnt<0>();
+#pragma unroll
+    for (int i = 0; i <= BDP; ++i) tie(L[i]);
+    tie_cols();
+    if constexpr (BDP == 2) {
+        for (int wfirst = w0; wfirst < wend; wfirst += FBC) {
+            const int nsteps = min(FBC, wend - wfirst);  // FBC = a multiple of BDP + 1: blocks start on L[0]
+            const bool fl = wfirst > w0;
             for (int s = 0; s < nsteps; s += 3) {
                 step(L[0], L[2], wfirst + s, s, fl);
                 if (s + 1 >= nsteps) break;
@@ -632,15 +646,42 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
                 if (s + 2 >= nsteps) break;
                 step(L[2], L[1], wfirst + s + 2, s + 2, fl);
             }
-        } else {
-            for (int s = 0; s < nsteps; s += 2) {
-                step(L[0], L[1], wfirst + s, s, fl);
-                if (s + 1 >= nsteps) break;
-                step(L[1], L[0], wfirst + s + 1, s + 1, fl);
-            }
+            reduce_to(nsteps - 1);
+            flush(wfirst, nsteps);
         }
-        reduce_to(nsteps - 1);
-        flush(wfirst, nsteps);
+    } else {
+        // Full blocks (FBC steps, FBC even: a block starts and ends on L[0]), then the last, shorter
+        // one.  No exit of the full-block loop depends on a step count, so the compiler's control-flow
+        // graph has no path from a block that ended on an odd step into the next block (on such a path
+        // it may take the pending L[1] loads as dead and reuse their registers, vmcnt_check.py).
+        static_assert(FBC % 2 == 0, "a full block ends on L[0]");
+        int wfirst = w0;
+        for (; wfirst + FBC <= wend; wfirst += FBC) {
+            step(L[0], L[1], wfirst, 0, std::true_type{});
+            for (int s = 1; s < FBC - 1; s += 2) {
+                step(L[1], L[0], wfirst + s, s, std::false_type{});
+                step(L[0], L[1], wfirst + s + 1, s + 1, std::false_type{});
+            }
+            step(L[1], L[0], wfirst + FBC - 1, FBC - 1, std::false_type{});
+            reduce_to(FBC - 1);
+            flush(wfirst, FBC);
+        }
+        // (the last step's loads have landed where the two paths below join: the compiler joins them
+        // with register copies too -- of loads past the segment's end, dead, but kept provable)
+        asm_vmcnt<0>();
+        tie(L[0]);
+        tie_cols();
+        if (wfirst < wend) {
+            const int nsteps = wend - wfirst;
+            step(L[0], L[1], wfirst, 0, std::true_type{});
+            for (int s = 1; s < nsteps; s += 2) {
+                step(L[1], L[0], wfirst + s, s, std::false_type{});
+                if (s + 1 >= nsteps) break;
+                step(L[0], L[1], wfirst + s + 1, s + 1, std::false_type{});
+            }
+            reduce_to(nsteps - 1);
+            flush(wfirst, nsteps);
+        }
     }
     // The last steps' prefetches are still in flight: keep their registers live (the compiler
     // would otherwise reuse them in the last flush) until they have landed.
@@ -949,6 +990,73 @@ __device__ __forceinline__ double gather_sum(const Geo& g, const BwdArgs& a, con
     return s;
 }
 
+// The remainder diagonal's term of type 3 side + q at pixel (y, x) (BwdArgs::remT / remT1, k_bwd_rem_rows).
+__device__ __forceinline__ double rem_term(const Geo& g, const BwdArgs& a, const float* remT, const float* remT1,
+                                           int side, int q, int64_t y, int64_t x) {
+    const int64_t nyw = (a.yhi - a.ylo) * g.W, nv = g.HV() * g.WO, yy = y - a.ylo, D = g.D;
+    if (q == 0) {
+        if (side == 0 ? x < g.WO + (g.k - 1 - g.r) : x >= D - g.r) return (double)remT1[side * nyw + yy * g.W + x];
+        return 0.0;
+    }
+    const int64_t w = side == 0 ? x : x - D;
+    if (y >= g.h_lo && y < g.h_hi && w >= 0 && w < g.WO) return (double)remT[(2 * side + q - 1) * nv + (y - g.h_lo) * g.WO + w];
+    return 0.0;
+}
+
+// The three sums of one side at pixel p when every cover list holds <= 8 slots (a.S <= 8: window layouts
+// up to four diagonal chunks): the lists first (4 dwords each; the camera side's three types share one
+// list, the projector's Ac / Bp another), then every slot value of the three types at once (zero past a
+// list's count), then the same fp64 sums in the same order as gather_sum (even / odd accumulators, list
+// order; the zero terms leave them unchanged) -- three dependent memory round trips per pixel instead of
+// one per slot pair.
+__device__ __forceinline__ void gather_sums8(const Geo& g, const BwdArgs& a, const float* remT, const float* remT1,
+                                             int side, int64_t y, int64_t x, int64_t p, double* s) {
+    const int64_t plane = g.H * g.W;
+    const unsigned short* list = (const unsigned short*)(a.cover + 3 * g.W);
+    const int nw = a.S >> 1;  // dwords per list (S is even)
+    int nq[3];
+    uint32_t lw[3][4];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int cls = side == 0 ? 0 : (q == 0 ? 1 : 2);
+        if (q > 0 && (side == 0 || q == 2)) {  // the same list as the previous type
+            nq[q] = nq[q - 1];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) lw[q][w] = lw[q - 1][w];
+            continue;
+        }
+        nq[q] = a.cover[cls * g.W + x];
+        const uint32_t* lp = (const uint32_t*)(list + ((size_t)cls * g.W + x) * a.S);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) lw[q][w] = w < nw ? lp[w] : 0u;
+    }
+    float v[3][8];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const float* base = a.part + (size_t)(3 * side + q) * a.S * plane + p;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t sl = (lw[q][i >> 1] >> (16 * (i & 1))) & 0xffffu;
+            v[q][i] = i < nq[q] ? base[(size_t)sl * plane] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        if (nq[q] < 0) {  // more slots than planned (k_bwd_cover): fail loudly
+            s[q] = __builtin_nan("");
+            continue;
+        }
+        double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            v0 += (double)v[q][i];
+            v1 += (double)v[q][i + 1];
+        }
+        s[q] = v0 + v1;
+        if (remT) s[q] += rem_term(g, a, remT, remT1, side, q, y, x);
+    }
+}
+
 // Per-pixel sums (k_bwd_gather -> k_bwd_combine3): fp64 sums of the fp32 chunk partials, stored as
 // fp32 (one more rounding of values that are sums of fp32 partials already; the box filters and the
 // final combination stay fp64).
@@ -957,7 +1065,7 @@ typedef float acc_t;
 // Sum the partial slots per pixel; out ([2 sides][3][H][W]): T1, Z = Am|Ac - m' B|Bp, B|Bp (k_bwd_combine3
 // forms no patch sums: the gather forms m' B as it loads its tile -- the same product, one fp64 array less
 // through HBM).
-template <typename T>
+template <typename T, bool S8 = false>
 __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, acc_t* acc, const float* remT,
                                                     const float* remT1) {
     // blockIdx.y = the image row, x = the column, z = the side (no 64-bit division per thread)
@@ -968,8 +1076,12 @@ __global__ __launch_bounds__(256) void k_bwd_gather(Geo g, BwdArgs a, acc_t* acc
     const int side = blockIdx.z;
     double s[3] = {0.0, 0.0, 0.0};
     if (y >= a.ylo && y < a.yhi) {
+        if constexpr (S8) {
+            gather_sums8(g, a, remT, remT1, side, y, x, p, s);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) s[q] = gather_sum(g, a, remT, remT1, side, q, y, x, p);
+            for (int q = 0; q < 3; ++q) s[q] = gather_sum(g, a, remT, remT1, side, q, y, x, p);
+        }
     }
     // Z = A - m' B (m' = box / k^2 - shift, the pixel's shifted patch mean): k_bwd_combine3 then
     // needs two box filters, Box[Z] = Box[A] - Box[m' B], and no patch sums
@@ -1098,6 +1210,12 @@ __global__ __launch_bounds__(256) void k_img_shift(const double* __restrict__ bs
 // zero-padded (out-of-image) load minus the shift gives the shifted padding value -cbar / -pbar.
 
 constexpr int kSumBlocks = 512;
+
+// CUSTMA_BWD_GATHER8=0 keeps the per-slot-pair gather loop everywhere (same-box A/B)
+inline bool gather8_enabled() {
+    const char* e = getenv("CUSTMA_BWD_GATHER8");
+    return !(e && e[0] == '0');
+}
 
 inline size_t a256(size_t n) { return (n + 255) & ~(size_t)255; }
 
@@ -1302,8 +1420,13 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     // halo -- measured slower: C5 backward op 29.5 -> 31.1 ms, C2 full 3.82 -> 3.95 ms)
     // (a column-wise form, cover lists staged in LDS once per 64 columns and each slot read for 4-8 rows at
     // once, measured slower: C5 1.82 -> 2.52-2.74 ms at 122-134 VGPRs against this kernel's 30)
-    hipLaunchKernelGGL(k_bwd_gather<T>, dim3((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2), dim3(256), 0, s, g, a, acc,
-                       a.remT, a.remT1);
+    {
+        const dim3 ggrid((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2);
+        if (p.S <= 8 && gather8_enabled())
+            hipLaunchKernelGGL((k_bwd_gather<T, true>), ggrid, dim3(256), 0, s, g, a, acc, a.remT, a.remT1);
+        else
+            hipLaunchKernelGGL((k_bwd_gather<T, false>), ggrid, dim3(256), 0, s, g, a, acc, a.remT, a.remT1);
+    }
     {
         constexpr int TS3 = 32;
         const int L3 = TS3 + g.k - 1;

@@ -297,6 +297,17 @@ __device__ __forceinline__ void asm_vmcnt() {
     static_assert(N >= 0 && N <= 63, "vmcnt field");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// N vector-memory stores that write nothing (offset past the descriptor's range): they stand in for a
+// step's N real stores where a hand-counted `s_waitcnt vmcnt` expects them in flight (inline asm, so
+// the compiler neither merges nor drops them; each with its own `s_nop 4` for a VALU-written SGPR of r,
+// as the compiler may restore r from VGPR lanes between them -- a few cycles, once per row band)
+template <int N>
+__device__ __forceinline__ void asm_null_stores(i32x4 r) {
+    const uint32_t oob = 0x80000000u, z = 0u;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        asm volatile("s_nop 4\n\tbuffer_store_dword %0, %1, %2, 0 offen" ::"v"(z), "v"(oob), "s"(r) : "memory");
+}
 template <typename V>
 __device__ __forceinline__ void asm_tie(V& v) {
     asm volatile("" : "+v"(v));

@@ -262,6 +262,28 @@ __device__ __forceinline__ void stats_tile(const T* __restrict__ img0, const T* 
     for (int p = 0; p < PR; ++p) {
         const int64_t y = y0 + ly0 + p;
         if (y >= yend) break;
+        // the thread's two columns as one 8- / 16-byte store where both lie in the image and the
+        // addresses are aligned (W even and 256-byte aligned planes, as the library carves them): half
+        // the store instructions, each lane's bytes contiguous
+        const int64_t xp = x0 + lx0, op = y * g.W + xp;
+        const bool al = (((uintptr_t)(st.sq + op) | (uintptr_t)(st.mean + op) | (uintptr_t)(st.sqt + op)) & 7) == 0 &&
+                        ((uintptr_t)(st.box + op) & 15) == 0;
+        if (!SC1 && (g.W & 1) == 0 && xp + 1 < g.W && al) {
+            static_assert(PC == 2, "column pairs");
+            if constexpr (MODE == STATS_FULL || MODE == STATS_MSB) *(f32x2*)(st.mean + op) = f32x2{m[p][0], m[p][1]};
+            *(f32x2*)(st.sq + op) = f32x2{sq[p][0], sq[p][1]};
+            *(f64x2*)(st.box + op) = f64x2{bx[p][0], bx[p][1]};
+            if constexpr (MODE == STATS_FULL) {
+                float t[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const double c2 = b2[p][c] - bx[p][c] * bx[p][c] / (double)(k * k);
+                    t[c] = (float)(c2 > 0.0 ? c2 : 0.0);
+                }
+                *(f32x2*)(st.sqt + op) = f32x2{t[0], t[1]};
+            }
+            continue;
+        }
 #pragma unroll
         for (int c = 0; c < PC; ++c) {
             const int64_t x = x0 + lx0 + c;

@@ -198,18 +198,24 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     // issues, so a peeled prologue with another register assignment would be joined to the
     // loop by register copies -- reads of registers whose loads are still in flight.
     Stage st[P];
-    auto compute = [&](Stage& p, int64_t t) {
+    // stores per step (every thread issues exactly ST: the hand-counted waits rely on it)
+    constexpr int ST = AMX > 0 ? (SOFT ? 5 : 3) * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);
+    static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
+    // out_c: std::true_type for an output step (t >= h0: stores), std::false_type for a warm-up step
+    // (P == 2: both fixed at compile time, so the waits are too); a runtime bool with P == 3
+    auto compute = [&](Stage& p, int64_t t, auto out_c) {
+        const bool out = out_c;
         // loads(t) were issued at the end of step t-P; after them, for each step s in
         // t-P+1 .. t-1: its stores (from step h0 on) and loads(s+P)
-        constexpr int ST = AMX > 0 ? (SOFT ? 5 : 3) * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);
-        static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
         if constexpr (P == 3) {
             if (t - 2 >= h0) asm_vmcnt<2 * (kLoads + ST)>();
             else if (t - 1 >= h0) asm_vmcnt<2 * kLoads + ST>();
             else asm_vmcnt<2 * kLoads>();
+        } else if constexpr (std::is_same<decltype(out_c), std::true_type>::value) {
+            // the previous step stored (or, for t = h0, the null stores between the phases stand in)
+            asm_vmcnt<kLoads + ST>();
         } else {
-            if (t - 1 >= h0) asm_vmcnt<kLoads + ST>();
-            else asm_vmcnt<kLoads>();
+            asm_vmcnt<kLoads>();
         }
         tie(p);
         rowE[l] = raw_to_f64<T>(p.pe0);
@@ -290,7 +296,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             colR = __builtin_fma(cRe, *(const lds_vd*)(rowE + 64 + l), colR);
             colR = __builtin_fma(cRl, *(const lds_vd*)(rowL + 64 + l), colR);
         }
-        if (t >= h0) {
+        if (out) {
             const auto rOut = make_rsrc(orow, tile_bytes);
             orow += ostep;
             double s = col[0] + (double)kEps;  // E + eps: eps rides along the sliding sum
@@ -315,6 +321,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             // every lane of the chunk valid (all but a partial last chunk): unmasked stage writes,
             // no per-output exec branch
             const bool allv = d0 + 63 <= g.D;
+            // FULL_EDGE: the column base opaque per step, so that the per-row store offsets below are
+            // not hoisted out of the output loop (16 VGPRs held across it: 141 -> 169 VGPRs)
+            int64_t a0S = a0;
+            if constexpr (FULL_EDGE) asm volatile("" : "+v"(a0S));
             auto outputs = [&](auto masked_c) {
             constexpr bool MASKED = decltype(masked_c)::value;
             Unroll<0, TW>::run([&](auto mc) {
@@ -333,7 +343,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
                 uint32_t vo = vOut, so = (uint32_t)(m * sstep);
                 if constexpr (FULL_EDGE) {  // per-row mask; the whole offset in voffset
-                    vo = ((uint64_t)(a0 + m) < (uint64_t)g.W) ? (uint32_t)((a0 + m + m * DO) * 4) : OOB;
+                    vo = ((uint64_t)(a0S + m) < (uint64_t)g.W) ? (uint32_t)((a0S + m + m * DO) * 4) : OOB;
                     so = 0;
                 }
                 if constexpr (STAGED) {
@@ -367,7 +377,12 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 // every wave's part of the 16 rows is in LDS: store the block (256 contiguous
                 // bytes per wave instruction, the whole workgroup's instruction contiguous)
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                const int NT = (int)blockDim.x, tid = (int)threadIdx.x;
+                const int NT = (int)blockDim.x;
+                // opaque per step: the block's store offsets are recomputed at each step instead of
+                // hoisted out of the output loop, where they would hold SS VGPRs across it (141 -> 166-171
+                // VGPRs, two waves per SIMD instead of three)
+                int tid = (int)threadIdx.x;
+                asm volatile("" : "+v"(tid));
                 const int total = (int)(nrow * DO);
                 if constexpr (AMX > 0) {
                     const int wv = tid >> 6, nw = NT >> 6, sub = l & 15;
@@ -453,25 +468,64 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             }
         }
     };
-    auto step = [&](auto kc, int64_t t) {
+    // comp: compute the step (false: the first P steps, which only issue loads); P == 2 passes
+    // compile-time constants throughout, so no step has a runtime test around its compute
+    auto step = [&](auto kc, int64_t t, auto out_c, auto comp) {
         Stage& p = st[decltype(kc)::value];
-        if (t >= hs) compute(p, t);
+        if (comp) compute(p, t, out_c);
         // past the band's end: harmless (rows out of range read zeros)
         load_step(t + P, p);
     };
-    int64_t t_first = hs - P;  // opaque: the warm-up iterations must not be peeled
-    asm volatile("" : "+s"(t_first));
-    for (int64_t t = t_first;; t += P) {
-        step(std::integral_constant<int, 0>{}, t);
-        if (t + 1 >= h1) break;
-        step(std::integral_constant<int, 1>{}, t + 1);
-        if (t + 2 >= h1) break;
-        if constexpr (P == 3) {
-            step(std::integral_constant<int, 2 % P>{}, t + 2);
+    const std::true_type yes{};
+    const std::false_type no{};
+    if constexpr (P == 2) {
+        // Three phases, every wait fixed at compile time, so that vmcnt_check.py can prove them on the
+        // emitted code (a runtime choice between two waits, a runtime test around a step's compute, or a
+        // `break` after each step gives paths the hardware never takes, on which the proof fails):
+        //   t = hs - 2, hs - 1:  loads only;
+        //   t = hs .. h0 - 1:    the K - 1 warm-up steps, no stores;
+        //   t = h0 .. h1 - 1:    ST stores per step -- pairs with the loop's only exit at its test, then
+        //                        an odd last step; ST null stores before it stand in for the stores of
+        //                        the step before t = h0.
+        // The stage buffers alternate throughout: the output phase starts on st[(K - 1) % 2].
+        constexpr int A = (K - 1) % 2;
+        int64_t t = hs - 2;
+        asm volatile("" : "+s"(t));  // (opaque: the load-only steps stay one issue each)
+        step(std::integral_constant<int, 0>{}, t, no, no);
+        step(std::integral_constant<int, 1>{}, t + 1, no, no);
+        t += 2;
+#pragma unroll 1
+        for (int i = 0; i < (K - 1) / 2; ++i, t += 2) {
+            step(std::integral_constant<int, 0>{}, t, no, yes);
+            step(std::integral_constant<int, 1>{}, t + 1, no, yes);
+        }
+        if constexpr (A == 1) {
+            step(std::integral_constant<int, 0>{}, t, no, yes);
+            ++t;
+        }
+        asm_null_stores<ST>(dCam);
+        for (; t + 1 < h1; t += 2) {
+            step(std::integral_constant<int, A>{}, t, yes, yes);
+            step(std::integral_constant<int, 1 - A>{}, t + 1, yes, yes);
+        }
+        if (t < h1) step(std::integral_constant<int, A>{}, t, yes, yes);
+    } else {
+        int64_t t_first = hs - P;  // opaque: the warm-up iterations must not be peeled
+        asm volatile("" : "+s"(t_first));
+        for (int64_t t = t_first;; t += P) {
+            step(std::integral_constant<int, 0>{}, t, t >= h0, t >= hs);
+            if (t + 1 >= h1) break;
+            step(std::integral_constant<int, 1>{}, t + 1, t + 1 >= h0, t + 1 >= hs);
+            if (t + 2 >= h1) break;
+            step(std::integral_constant<int, 2 % P>{}, t + 2, t + 2 >= h0, t + 2 >= hs);
             if (t + 3 >= h1) break;
         }
     }
     asm_vmcnt<0>();  // every wave drains its own loads before it ends
+    // The last steps' loads (rows past the band) are dead, but their registers must not be reused
+    // before they land -- a late load would overwrite the new value: keep them live until here.
+#pragma unroll
+    for (int i = 0; i < P; ++i) tie(st[i]);
 }
 
 template <int K, typename T>
@@ -520,11 +574,17 @@ constexpr int kWaveLds = (3 * kRowP + 64) * 8 + kRowP * 4;  // rowE, rowL, sM, s
 // waits only for tiles of LOWER hardware index, so the grid cannot deadlock whatever the placement
 // (blocks start in index order); the poll is bounded, never a hang.
 constexpr int kFusedMinK = 3;
+// CUSTMA_FWD_FUSED=2: the sweep tiles take one agent-scope acquire after their poll and read the
+// statistics with plain loads (=1: `sc1` loads, no acquire)
+inline bool fused_acquire() {
+    const char* e = getenv("CUSTMA_FWD_FUSED");
+    return e && e[0] == '2';
+}
 struct FusedGrid {
     int nBand, nTile, nSC, P, perX, len;  // P = 2 nSC statistics tiles per band; perX bands per XCD
 };
 
-template <int K, typename T, bool X4, int AMX = 0, bool CPL = false, bool FUSED = false>
+template <int K, typename T, bool X4, int AMX = 0, bool CPL = false, bool FUSED = false, bool FUSED_ACQ = false>
 __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __restrict__ cam,
                                                                  const T* __restrict__ proj, Geo g, Stats sc,
                                                                  Stats sp, float* __restrict__ out, WaveGrid wg,
@@ -567,10 +627,16 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
             if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + sb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
-        if (threadIdx.x == 0) {  // wait for the band's statistics (bounded: ~0.5 s, then go on)
+        if (threadIdx.x == 0) {  // wait for the band's statistics (bounded: ~0.2 s, then go on)
             for (int it = 0; it < (1 << 20); ++it) {
                 if (__hip_atomic_load(cnt + band, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= fg.P) break;
                 __builtin_amdgcn_s_sleep(8);
+            }
+            // FUSED_ACQ: one agent-scope acquire (this CU's L1 invalidated), then the statistics are read
+            // with plain loads; else every statistics load is an `sc1` load
+            if constexpr (FUSED_ACQ) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
         __syncthreads();
@@ -595,13 +661,13 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
     constexpr int kTP = X4 ? kTileP : 2;  // deeper pipelines only with the 16-byte stores (vmcnt range)
     if (!wg.rem)
-        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                          rowL, sM, sQ, sR, stage, part, camL);
     else if (w == wg.nChunk - 1)
-        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                         rowL, sM, sQ, sR, stage, part, camL);
     else
-        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL, FUSED>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                          rowL, sM, sQ, sR, stage, part, camL);
 }
 
@@ -678,17 +744,22 @@ hipError_t launch_fused(const T* cam, const T* proj, const Geo& g, Stats sc, Sta
     if (e != hipSuccess) return e;
     const dim3 grid((unsigned)(8 * (int64_t)fg.len)), blk(64 * wg.nChunk);
     prof_begin(PROF_FWD, s);
+    auto go = [&](auto cpl_, auto acq_) -> hipError_t {
+        constexpr bool CPLV = decltype(cpl_)::value, ACQ = decltype(acq_)::value;
+        hipError_t r = allow_lds(k_fwd_tile<K, T, true, 0, CPLV, true, ACQ>, lds);
+        if (r != hipSuccess) return r;
+        hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, CPLV, true, ACQ>), grid, blk, lds, s, cam, proj, g, sc, sp, out,
+                           wg, DispPartial{}, cnt, fg);
+        return hipSuccess;
+    };
+    const bool acq = fused_acquire();
     if (cpl) {
-        if constexpr (sizeof(T) == 2) {
-            if ((e = allow_lds(k_fwd_tile<K, T, true, 0, true, true>, lds)) != hipSuccess) return e;
-            hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, true, true>), grid, blk, lds, s, cam, proj, g, sc, sp, out, wg,
-                               DispPartial{}, cnt, fg);
-        }
+        if constexpr (sizeof(T) == 2)
+            e = acq ? go(std::true_type{}, std::true_type{}) : go(std::true_type{}, std::false_type{});
     } else {
-        if ((e = allow_lds(k_fwd_tile<K, T, true, 0, false, true>, lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, false, true>), grid, blk, lds, s, cam, proj, g, sc, sp, out, wg,
-                           DispPartial{}, cnt, fg);
+        e = acq ? go(std::false_type{}, std::true_type{}) : go(std::false_type{}, std::false_type{});
     }
+    if (e != hipSuccess) return e;
     prof_end(PROF_FWD, s);
     return hipGetLastError();
     }
@@ -783,7 +854,7 @@ bool fused_forward_ok(const Geo& g, const void* out) {
     // opt-in (CUSTMA_FWD_FUSED=1): measured slower than the separate statistics pass + one sweep
     // (same-process A/B/C, profiles/r05/a/ab_split.log: C3 1.030 vs 0.998 ms, C5 9.56 vs 9.35 ms)
     const char* e = getenv("CUSTMA_FWD_FUSED");
-    if (!e || e[0] != '1') return false;
+    if (!e || (e[0] != '1' && e[0] != '2')) return false;
     if (g.layout != CUSTMA_LAYOUT_WINDOW || g.W % 32 != 0 || g.band_rows > 0 || g.k < 3) return false;
     const WaveGrid wg = wave_grid(g);
     const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0);

@@ -24,6 +24,7 @@ Tests on CPU (gloo) inject the oracle as the backend; the product never does.
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import Optional, Tuple
 
@@ -66,8 +67,8 @@ _TIMING = {"on": False, "events": []}
 
 def enable_timing(on: bool = True) -> None:
     """Record, per exchange, the time the op's stream waited for it (device tensors only):
-    ``fwd_exposed`` = from the end of the interior-row forward launch to the halo's arrival
-    (zero when the exchange hid behind that compute), ``bwd`` = the whole halo reduce."""
+    ``fwd_exposed`` = from the post of the exchange (CUSTMA_ROWBAND_OVERLAP=1: from the end of the
+    interior-row forward launch) to the halo's arrival, ``bwd`` = the whole halo reduce."""
     _TIMING["on"] = on
     _TIMING["events"] = []
 
@@ -258,16 +259,32 @@ def _forward_band(backend, ch, ph, D, k, layout, precision, lo, hi, vol, top):
         dst.copy_(backend.forward(ch, ph, D, k, layout, precision, (top + lo, top + hi)))
 
 
+# The forward of a band with halos: by default the halos land first and the band is ONE forward (one
+# statistics pass, one sweep launch).  CUSTMA_ROWBAND_OVERLAP=1 computes the interior rows while the
+# halos are in flight and the two edges afterwards -- three statistics passes and three sweeps per rank,
+# the edge sweeps shorter than their k - 1 warm-up rows; at C5 / 8 ranks the exchange is ~330 KB, a few
+# microseconds over xGMI, less than the two extra launch pairs.
+def _overlap_interior() -> bool:
+    return os.environ.get("CUSTMA_ROWBAND_OVERLAP", "0") == "1"
+
+
 class _RowBandStereoMatching(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cam_band, proj_band, D, kernel_size, layout, precision, rbg, backend):
-        # Post both images' halo exchanges, compute the interior volume rows (patches inside the
-        # owned rows) while they are in flight, then the edge rows once the halos have landed.
+        # Post both images' halo exchanges; then either wait for them and run one band forward, or
+        # (CUSTMA_ROWBAND_OVERLAP=1) compute the interior volume rows (patches inside the owned rows) while they
+        # are in flight and the edge rows once the halos have landed.
         ch, pc = rbg.exchange_halo_start(cam_band.contiguous())
         ph, pp = rbg.exchange_halo_start(proj_band.contiguous())
         top, _ = rbg.halo_sizes()
         n = cam_band.shape[0]
         if pc is None:
+            vol = backend.forward(ch, ph, D, kernel_size, layout, precision, (top, top + n))
+        elif not _overlap_interior():
+            e0 = _event(cam_band)
+            pc.wait()
+            pp.wait()
+            _record("fwd_exposed", e0, cam_band)
             vol = backend.forward(ch, ph, D, kernel_size, layout, precision, (top, top + n))
         else:
             W = ch.shape[1]

@@ -1,5 +1,6 @@
 """Same-process interleaved A/B/C of the forward's three forms at C3 and C5 window: the fused launch
-(CUSTMA_FWD_FUSED=1: statistics tiles inside the sweep's grid), the split forward (CUSTMA_FWD_SPLIT=1: two
+(CUSTMA_FWD_FUSED=1: statistics tiles inside the sweep's grid, `sc1` statistics loads; =2: one acquire per
+sweep tile and plain loads), the split forward (CUSTMA_FWD_SPLIT=1: two
 half-band sweeps on two streams) and the single stream (the default: the statistics pass, then one sweep);
 both switches are read per call.  Forward op time from HIP events around the op; every form's volume must
 equal the first one's bit for bit.  Usage: python scripts/ab_split.py [rounds]"""
@@ -15,7 +16,8 @@ import custereomatching_amd as cm  # noqa: E402
 from bench import EventTimer, synth_pair  # noqa: E402
 from kbench import CFGS, warm  # noqa: E402
 
-FORMS = {"fused": {"CUSTMA_FWD_FUSED": "1"}, "split": {"CUSTMA_FWD_SPLIT": "1"}, "single": {}}
+FORMS = {"fused": {"CUSTMA_FWD_FUSED": "1"}, "fused_acq": {"CUSTMA_FWD_FUSED": "2"}, "split": {"CUSTMA_FWD_SPLIT": "1"},
+         "single": {}}
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 for name in ("c3_win", "c5_win"):
     c = CFGS[name]

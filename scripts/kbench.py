@@ -23,6 +23,10 @@ CFGS = {
     "c3_win_k19": dict(H=2048, W=2048, k=19, D=256, layout="window", dtype=torch.float16),
     "c3_win_k25": dict(H=2048, W=2048, k=25, D=256, layout="window", dtype=torch.float16),
     "c3_win_k31": dict(H=2048, W=2048, k=31, D=256, layout="window", dtype=torch.float16),
+    "c3_win_k18": dict(H=2048, W=2048, k=18, D=256, layout="window", dtype=torch.float16),
+    "c3_win_k22": dict(H=2048, W=2048, k=22, D=256, layout="window", dtype=torch.float16),
+    "c3_win_k30": dict(H=2048, W=2048, k=30, D=256, layout="window", dtype=torch.float16),
+    "c3_full_k19": dict(H=2048, W=2048, k=19, D=256, layout="full", dtype=torch.float16),
     # other sweep kernel sizes at C3 size
     "c3_win_k5": dict(H=2048, W=2048, k=5, D=256, layout="window", dtype=torch.float16),
     "c3_win_k9": dict(H=2048, W=2048, k=9, D=256, layout="window", dtype=torch.float16),

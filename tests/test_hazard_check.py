@@ -79,6 +79,8 @@ def test_shipped_backward_listing_is_clean(tmp_path):
                         "--cuda-device-only", "-S", src, "-o", str(out)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     assert hc.main(["hazard_check.py", str(out)]) == 0
+    import vmcnt_check  # the same listing: no register read with its load in flight (tests/test_vmcnt_check.py)
+    assert vmcnt_check.main(["vmcnt_check.py", str(out)]) == 0
 
 
 def test_build_rejects_scratch_use():

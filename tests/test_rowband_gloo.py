@@ -48,7 +48,8 @@ class OracleBackend:
         return torch.from_numpy(idx), torch.from_numpy(best)
 
 
-def _worker(rank, world, port, H, W, k, D, layout, q, pass_h=False, split=None):
+def _worker(rank, world, port, H, W, k, D, layout, q, pass_h=False, split=None, overlap=False):
+    os.environ["CUSTMA_ROWBAND_OVERLAP"] = "1" if overlap else "0"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -74,11 +75,11 @@ def _worker(rank, world, port, H, W, k, D, layout, q, pass_h=False, split=None):
         dist.destroy_process_group()
 
 
-def _run(world, H, W, k, D, layout, pass_h=False, split=None):
+def _run(world, H, W, k, D, layout, pass_h=False, split=None, overlap=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, k, D, layout, q, pass_h, split))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, H, W, k, D, layout, q, pass_h, split, overlap))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -89,12 +90,15 @@ def _run(world, H, W, k, D, layout, pass_h=False, split=None):
     return res
 
 
-@pytest.mark.parametrize("world,layout,k", [(2, "full", 5), (3, "window", 5), (2, "window", 5), (2, "full", 4),
-                                            (3, "window", 6), (2, "full", 2), (3, "full", 1)])
-def test_rowband_matches_single_device(world, layout, k):
+@pytest.mark.parametrize("world,layout,k,overlap", [
+    (2, "full", 5, False), (3, "window", 5, False), (2, "window", 5, False), (2, "full", 4, False),
+    (3, "window", 6, False), (2, "full", 2, False), (3, "full", 1, False),
+    # CUSTMA_ROWBAND_OVERLAP=1: interior rows while the halos are in flight, then the two edges
+    (3, "window", 5, True), (2, "full", 4, True), (3, "full", 6, True)])
+def test_rowband_matches_single_device(world, layout, k, overlap):
     """Odd k: r halo rows each side; even k: k/2 rows from the rank above, k/2-1 from below."""
     H, W, D = 23, 28, 6
-    res = _run(world, H, W, k, D, layout)
+    res = _run(world, H, W, k, D, layout, overlap=overlap)
     cam, proj = make_pair(H, W, max(D, 1), seed=17)
     lay, Dl = OracleBackend._lay(layout, D)
     vol = O.forward(cam, proj, k, layout=lay, D=Dl)
