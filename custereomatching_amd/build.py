@@ -23,7 +23,7 @@ UNITS = [(os.path.splitext(src)[0], src, []) for src in SOURCES if src != "sweep
 UNITS += [("sweep_wave_d", "sweep_wave.hip", ["-DCUSTMA_SW_DISPATCH"])]
 UNITS += [(f"sweep_wave_k{k}", "sweep_wave.hip", [f"-DCUSTMA_SW_K={k}"]) for k in SWEEP_KS]
 # translation units whose inline asm omits wait states where the listing shows none are needed
-HAZARD_CHECKED = ("bwd_fused.hip", "sweep_wave.hip")
+HAZARD_CHECKED = ("bwd_fused.hip", "sweep_wave.hip", "sweep_fwd.hip")
 ARCH = os.environ.get("CUSTMA_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: fused multiply-adds only where written (__builtin_fmaf / fma);

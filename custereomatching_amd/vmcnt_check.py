@@ -136,12 +136,13 @@ def facts_transfer(facts, ins):
         for r in regs_of(ins.fields[0]):
             if r[0] == "s":
                 f[str(r[1])] = v
-    if op == "s_andn2_b64" and ins.fields[:2] == ["vcc", "exec"] and len(ins.fields) == 3:
-        vals = [f.get(str(r[1])) for r in regs_of(ins.fields[2]) if r[0] == "s"]
-        if vals and all(v == -1 for v in vals):
-            f["vccz"] = True  # exec & ~all-ones
-        elif vals and all(v == 0 for v in vals):
-            f["vccz"] = False  # exec (non-zero in any block that runs)
+    if op in ("s_andn2_b64", "s_and_b64") and len(ins.fields) == 3 and ins.fields[0] == "vcc" and \
+            "exec" in ins.fields[1:] and (op == "s_and_b64" or ins.fields[1] == "exec"):
+        other = ins.fields[2] if ins.fields[1] == "exec" else ins.fields[1]
+        vals = [f.get(str(r[1])) for r in regs_of(other) if r[0] == "s"]
+        if vals and all(v in (0, -1) for v in vals) and len(set(vals)) == 1:
+            # exec & ~mask / exec & mask; exec is non-zero in any block that runs
+            f["vccz"] = (vals[0] == -1) if op == "s_andn2_b64" else (vals[0] == 0)
     return frozenset(f.items())
 
 

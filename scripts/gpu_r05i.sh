@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 5 (i): HEAD evidence -- smoke, the row-band GPU tests (one-launch forward), a kernel trace of the
+# contract bench workload (c5) and of the C3 north star / disparity / backward, C2 full forward.
+set -o pipefail
+TAG=${1:-r05i}
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/$TAG
+mkdir -p $O
+md5sum custereomatching_amd/_lib/libcustma_hip.so
+fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit $1;; esac; }
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 $O/smoke.log; fatal $rc smoke
+timeout -k 10 400 python -u -m pytest tests/test_rowband_gpu.py -m gpu -q --timeout 120 --timeout-method thread > $O/rowband_gpu.log 2>&1
+rc=$?; echo "rowband rc=$rc"; grep -E "passed|failed|FAILED" $O/rowband_gpu.log | tail -5; fatal $rc rowband
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o run --output-format csv -- python3 bench.py --steps 5 --no-pmc --no-cpu-baseline > $O/bench_traced.json 2> $O/bench_traced.err
+rc=$?; echo "traced bench rc=$rc"; fatal $rc traced_bench
+cut -c1-300 $O/bench_traced.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o run --output-format csv -- python3 scripts/kbench.py --cfg c3_win --ops fwd,disp,bwd --reps 10 > $O/kbench_c3.log 2>&1
+rc=$?; echo "c3 trace rc=$rc"; grep cfg $O/kbench_c3.log; fatal $rc c3_trace
+timeout -k 10 300 python3 scripts/kbench.py --cfg c2_full,c3_full --ops fwd,disp --reps 5 > $O/kbench_full.log 2>&1
+rc=$?; echo "full rc=$rc"; grep cfg $O/kbench_full.log; fatal $rc full
+find $O -name "*kernel_stats.csv" | head
