@@ -86,6 +86,14 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     // and never load from HBM.  (vmcnt counts loads and stores in issue order, so a wave
     // doing both waits for its earlier volume stores whenever it consumes a load.)
     const bool loader = __builtin_amdgcn_readfirstlane(tid) >= NL;
+    if constexpr (ARGMAX) {
+        // the reduction rows' padding columns NL .. NLP - 1 (NLP below), ordered before the scans by barrier #0
+        int TPR = 1;
+        while (TPR * 2 * TWT <= NL && TPR < 16) TPR *= 2;
+        const int NLP = NL + TPR;
+        for (int e = tid; e < TWT * NLP; e += (int)blockDim.x)
+            if (e % NLP >= NL) stg[e] = -FLT_MAX;
+    }
     const double rk2 = 1.0 / (double)(K * K);
     constexpr uint32_t OOB = 0x80000000u;
 
@@ -359,15 +367,29 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 // layout index s of diagonal lane l for camera column u0 + m
                 const float sbase = (float)(window ? d0 : u0 + m + d0);
                 const float* rowp = stg + (red_live ? m : 0) * NLP;
+                // nsc steps for every lane, no bound test: the row's columns NL .. NLP - 1 hold -FLT_MAX
+                // (written once, below the loader split), which changes neither best, second nor bi.  So
+                // the LDS reads batch up instead of one exec-masked, waited read per element; the soft
+                // sums are a separate loop (their flag is uniform).  second never holds a NaN (it takes
+                // best, or v when v > second), so max(second, v) needs no fmaxf NaN handling.
+                const int nsc = (NL + TPR - 1) / TPR;
+                auto scan = [&](auto soft_c) {
+                    constexpr bool SOFTC = decltype(soft_c)::value;
 #pragma unroll 4
-                for (int l = part_i; l < NL; l += TPR) {
-                    const float v = red_live ? rowp[l] : -FLT_MAX;
-                    if (soft && v > -FLT_MAX) soft_add(v, sbase + (float)l, best, part.kb, q0, q1);
-                    const bool gt = v > best;
-                    second = gt ? best : fmaxf(second, v);
-                    bi = gt ? l : bi;
-                    best = gt ? v : best;
-                }
+                    for (int e = 0; e < nsc; ++e) {
+                        const int l = part_i + TPR * e;
+                        const float v = red_live ? rowp[l] : -FLT_MAX;
+                        if constexpr (SOFTC) {
+                            if (v > -FLT_MAX) soft_add(v, sbase + (float)l, best, part.kb, q0, q1);
+                        }
+                        const bool gt = v > best;
+                        second = gt ? best : (v > second ? v : second);
+                        bi = gt ? l : bi;
+                        best = gt ? v : best;
+                    }
+                };
+                if (soft) scan(std::true_type{});
+                else scan(std::false_type{});
                 auto merge = [&](auto ctl) {
                     constexpr int c = decltype(ctl)::value;
                     auto mv = [&](float x) {

@@ -74,6 +74,9 @@ constexpr int kFwdPF = 2;  // outputs whose projector statistics are read ahead 
 // (every wave needs the same ones) are loaded once into LDS (camL, zero-padded) before the sweep,
 // instead of four 16-address loads per wave and step: those loads were most of the sweep's load
 // cost (C5: 9.80 -> 8.25 ms with every camera load out of range, profiles/r03/fwdabl).
+// the fused disparity's stage row pitch: all D + 1 <= 64 kTileMaxChunks + 1 diagonals, rounded up to the
+// scan's 16 lanes (the columns past DO padded with -FLT_MAX)
+constexpr int kAmxPitch = 16 * ((64 * kTileMaxChunks + 1 + 15) / 16);
 template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2, int AMX_ = 0,
           bool CPL = false, bool SC1 = false>
 __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
@@ -316,7 +319,10 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 mq[i] = mrow[i];
                 qq[i] = qrow[i];
             });
-            lds_vf* sb = (lds_vf*)(stage + (t & 1) * TW * DO);  // STAGED: this step's buffer
+            // STAGED: this step's buffer; rows at pitch DO (the block the stores copy out), or at
+            // kAmxPitch with the fused disparity (the columns past DO hold -FLT_MAX, k_fwd_tile)
+            const int SPc = AMX > 0 ? kAmxPitch : (int)DO;
+            lds_vf* sb = (lds_vf*)(stage + (t & 1) * TW * SPc);
             const bool dv = d0 + l <= g.D;
             // every lane of the chunk valid (all but a partial last chunk): unmasked stage writes,
             // no per-output exec branch
@@ -347,7 +353,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                     so = 0;
                 }
                 if constexpr (STAGED) {
-                    if (!MASKED || dv) sb[m * DO + d0 + l] = c;
+                    if (!MASKED || dv) sb[m * SPc + d0 + l] = c;
                 } else
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, so,
                                                       kStoreAux);
@@ -366,7 +372,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 const float den2 = __builtin_fmaf(uq, *(const lds_vf*)(sQ + 64 + (l & 15)), kEps);
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
                 if constexpr (STAGED) {
-                    if (l < 16) sb[l * DO + g.D] = c;
+                    if (l < 16) sb[l * SPc + g.D] = c;
                 } else {
                     const uint32_t vo = l < 16 ? (uint32_t)((l * DO + g.D) * 4) : OOB;
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, 0u,
@@ -404,20 +410,24 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                         int bi = INT_MAX;
                         // increasing s per lane: the first index wins among equal values
                         const int mr = m < TW ? m : 0;
-                        // partly unrolled: fully unrolled, the compiler hoists all 17 LDS reads (and
-                        // the soft sums' exp2 operands) and the kernel needs 168-206 VGPRs; 6 (3 with
-                        // the soft sums) keeps every variant at 149-155 VGPRs, 3 waves per SIMD
+                        // No bound test: the row's columns DO .. 16 nsc - 1 hold -FLT_MAX, which changes
+                        // neither b, sec nor bi (b starts at -FLT_MAX, `gt` is strict), so the reads
+                        // batch up (an exec-masked read per element waited for each one: the scan was
+                        // 28 % of the kernel, profiles/r05/k).  sec never holds a NaN (it takes b, or v
+                        // when v > sec), so max(sec, v) needs no fmaxf NaN handling.  Partly unrolled:
+                        // fully unrolled, the compiler hoists all 17 LDS reads (and the soft sums' exp2
+                        // operands) and the kernel needs 168-206 VGPRs.
+                        const int nsc = ((int)DO + 15) >> 4;
+                        const lds_vf* row = sb + mr * kAmxPitch + sub;
 #pragma unroll SOFT ? 3 : 6
-                        for (int i = 0; i < (64 * kTileMaxChunks + 1 + 15) / 16; ++i) {
+                        for (int i = 0; i < nsc; ++i) {
                             const int s2 = sub + 16 * i;
-                            if (s2 < (int)DO) {
-                                const float v = sb[mr * DO + s2];
-                                if (soft) soft_add(v, (float)s2, b, kb, q0, q1);
-                                const bool gt = v > b;
-                                sec = gt ? b : fmaxf(sec, v);
-                                bi = gt ? s2 : bi;
-                                b = gt ? v : b;
-                            }
+                            const float v = row[16 * i];
+                            if (soft && v > -FLT_MAX) soft_add(v, (float)s2, b, kb, q0, q1);
+                            const bool gt = v > b;
+                            sec = gt ? b : (v > sec ? v : sec);
+                            bi = gt ? s2 : bi;
+                            b = gt ? v : b;
                         }
                         Unroll<0, 4>::run([&](auto lc) {
                             constexpr int ctrl = 0x120 + (8 >> decltype(lc)::value);  // row_ror:8, 4, 2, 1
@@ -656,6 +666,10 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     const int64_t u0 = (int64_t)wt * TW;
     const int64_t h0 = g.h_lo + (int64_t)band * wg.TH, h1 = min(g.h_hi, h0 + wg.TH);
     const int64_t d0 = (int64_t)w * 64;
+    if constexpr (AMX != 0) {  // the stage rows' padding columns (both buffers), once per workgroup
+        for (int e = (int)threadIdx.x; e < 2 * TW * kAmxPitch; e += (int)blockDim.x)
+            if (e % kAmxPitch >= (int)g.DO) stage[e] = -FLT_MAX;
+    }
     // SS stores per thread cover the 16 DO-float block: DO <= 64 nChunk, or 64 nChunk + 1 (rem);
     // X4: 4 (5 with rem) 16-byte stores per thread
     constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
@@ -771,7 +785,7 @@ hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats
     const WaveGrid wg = wave_grid(g);
     const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
     // (no camera preload here: it measured slower, C5 9.69 -> 9.99 ms, C3 1.15 -> 1.18 ms)
-    const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
+    const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)kAmxPitch * 4;
     prof_begin(PROF_FWD, s);
     const int passes = wg.nChunk == 4 ? 1 : wg.nChunk >= 2 ? 2 : 4;  // 16 rows over the waves, 4 per pass
     auto go = [&](auto amx) {
