@@ -340,6 +340,35 @@ __device__ __forceinline__ float ld_bufs<__half>(__amdgpu_buffer_rsrc_t r, uint3
 __device__ __forceinline__ double ld_bufs_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t so) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, so, 0));
 }
+// Zero-padded 2-D tile of an image into LDS (as float): image rows y0 .. y0 + ny - 1, columns
+// x0 .. x0 + nx - 1, at LDS row pitch `pitch`.  Raw buffer loads over the image rows from max(0, y0) on:
+// an element outside the image takes an out-of-range offset and reads 0 (the reference's zero padding,
+// stereo_matching_kernel.cu:6-12), so every load is unconditional and B of them per thread are in flight
+// together (a bounds-tested load per element -- ldpad -- was waited for one at a time).
+template <typename T, int B = 4>
+__device__ __forceinline__ void tile_to_lds(const T* img, int64_t H, int64_t W, int64_t y0, int64_t x0, int ny,
+                                            int nx, float* dst, int pitch, int tid, int nthreads) {
+    const int64_t yb = y0 > 0 ? y0 : 0;
+    const uint64_t nb = (uint64_t)(H > yb ? H - yb : 0) * (uint64_t)W * sizeof(T);
+    const auto r = make_rsrc(img + yb * W, nb < 0x7FFFFFF0u ? (uint32_t)nb : 0x7FFFFFF0u);
+    const int total = ny * nx;
+    for (int e0 = 0; e0 < total; e0 += B * nthreads) {
+        float v[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            const int e = e0 + tid + i * nthreads, ee = e < total ? e : 0;
+            const int ty = ee / nx, tx = ee - ty * nx;
+            const int64_t y = y0 + ty, x = x0 + tx;
+            const bool in = e < total && y >= 0 && y < H && x >= 0 && x < W;
+            v[i] = ld_bufs<T>(r, in ? (uint32_t)(((y - yb) * W + x) * (int64_t)sizeof(T)) : 0x80000000u, 0u);
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            const int e = e0 + tid + i * nthreads;
+            if (e < total) dst[(e / nx) * pitch + e % nx] = v[i];
+        }
+    }
+}
 // Cache-policy bits of the volume stores (gfx950: 1 sc0, 2 nt, 16 sc1).  nt (streaming): the
 // volume is written once and far exceeds L2 / MALL, and keeping it out of L2 leaves the
 // sweep's image-statistics rows there (C3 window tile kernel 1.26 -> 1.10 ms on MI355X).

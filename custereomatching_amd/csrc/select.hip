@@ -159,10 +159,8 @@ __global__ __launch_bounds__(256) void k_disp_merge_tile(const T* __restrict__ c
     float* tc = tl;
     float* tp = tl + CY * CX;
     const int64_t x0 = (int64_t)(blockIdx.x % ntx) * kMTX, hy0 = g.h_lo + (int64_t)(blockIdx.x / ntx) * kMTY;
-    for (int e = threadIdx.x; e < CY * CX; e += 256)
-        tc[e] = ldpad(cam, g.H, g.W, hy0 - R + e / CX, x0 - R + e % CX);
-    for (int e = threadIdx.x; e < CY * PX; e += 256)
-        tp[e] = ldpad(proj, g.H, g.W, hy0 - R + e / PX, x0 - R + e % PX);
+    tile_to_lds<T>(cam, g.H, g.W, hy0 - R, x0 - R, CY, CX, tc, CX, (int)threadIdx.x, 256);
+    tile_to_lds<T>(proj, g.H, g.W, hy0 - R, x0 - R, CY, PX, tp, PX, (int)threadIdx.x, 256);
     __syncthreads();
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int64_t h = hy0 + ty, w = x0 + tx;

@@ -90,6 +90,20 @@ inline float ldpad(const T* img, int64_t H, int64_t W, int64_t y, int64_t x) {
     return (y < 0 || y >= H || x < 0 || x >= W) ? 0.f : to_f(img[y * W + x]);
 }
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+// raw buffer loads: an access past num_records reads 0 (the gfx950 range check)
+struct EmuRsrc {
+    const char* base;
+    uint32_t n;
+};
+inline EmuRsrc make_rsrc(const void* base, uint32_t bytes) { return EmuRsrc{(const char*)base, bytes}; }
+template <typename T>
+inline float ld_bufs(EmuRsrc r, uint32_t off, uint32_t so) {
+    const uint64_t o = (uint64_t)off + so;
+    if (o + sizeof(T) > r.n) return 0.f;
+    T v;
+    memcpy(&v, r.base + o, sizeof(T));
+    return to_f(v);
+}
 hipError_t launch_stats(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, hipStream_t s,
                         int mode, float* prep, const float* shift, int rows);
 }  // namespace custma
