@@ -1030,14 +1030,19 @@ __device__ __forceinline__ void gather_sums8(const Geo& g, const BwdArgs& a, con
 #pragma unroll
         for (int w = 0; w < 4; ++w) lw[q][w] = w < nw ? lp[w] : 0u;
     }
+    // every slot load unconditional (a raw buffer load per type, past the list's count an out-of-range
+    // offset reads 0): a bounds-tested load per slot was waited for one at a time.  A type's S slot
+    // planes stay below 2 GiB (run_bwd picks this form only then), so a 32-bit offset reaches them.
     float v[3][8];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-        const float* base = a.part + (size_t)(3 * side + q) * a.S * plane + p;
+        const uint64_t tb = (uint64_t)a.S * (uint64_t)plane * 4u;
+        const auto rq = make_rsrc(a.part + (size_t)(3 * side + q) * a.S * plane, tb < 0x7FFFFFF0u ? (uint32_t)tb : 0x7FFFFFF0u);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t sl = (lw[q][i >> 1] >> (16 * (i & 1))) & 0xffffu;
-            v[q][i] = i < nq[q] ? base[(size_t)sl * plane] : 0.f;
+            const uint32_t off = i < nq[q] ? (uint32_t)(((uint64_t)sl * (uint64_t)plane + (uint64_t)p) * 4u) : 0x80000000u;
+            v[q][i] = ld_bufs<float>(rq, off, 0u);
         }
     }
 #pragma unroll
@@ -1422,7 +1427,9 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     // once, measured slower: C5 1.82 -> 2.52-2.74 ms at 122-134 VGPRs against this kernel's 30)
     {
         const dim3 ggrid((unsigned)cdiv(g.W, 256), (unsigned)g.H, 2);
-        if (p.S <= 8 && gather8_enabled())
+        // (the batched form's 32-bit buffer offsets reach one type's S partial planes while they stay
+        // below 2 GiB; larger images take the per-slot-pair form)
+        if (p.S <= 8 && gather8_enabled() && (double)p.S * (double)n * 4.0 < 2147483648.0)
             hipLaunchKernelGGL((k_bwd_gather<T, true>), ggrid, dim3(256), 0, s, g, a, acc, a.remT, a.remT1);
         else
             hipLaunchKernelGGL((k_bwd_gather<T, false>), ggrid, dim3(256), 0, s, g, a, acc, a.remT, a.remT1);
