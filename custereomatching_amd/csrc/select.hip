@@ -92,6 +92,40 @@ __device__ float exact_cost(const T* cam, const T* proj, const Geo& g, const Sta
     return (e + kEps) / den;
 }
 
+// exact_cost for any k with the patch loads batched: per patch row, 8 camera and 8 projector values
+// through unconditional raw buffer loads (out-of-image offsets read 0, as ldpad) in flight together,
+// then the same fma chain in the same order (the taps past k are loaded but not used).  A bounds-tested
+// load per tap was waited for one at a time: 2 k^2 round trips per voxel in k_disp_recheck.
+template <typename T>
+__device__ float exact_cost_batched(const T* cam, const T* proj, const Geo& g, const Stats& sc, const Stats& sp,
+                                    int64_t h, int64_t w, int64_t d) {
+    const uint64_t nb = (uint64_t)g.H * (uint64_t)g.W * sizeof(T);
+    if (nb >= 0x7FFFFFF0u) return exact_cost<T>(cam, proj, g, sc, sp, h, w, d);
+    const auto rc = make_rsrc(cam, (uint32_t)nb), rp = make_rsrc(proj, (uint32_t)nb);
+    const float mc = sc.mean[h * g.W + w], mp = sp.mean[h * g.W + d];
+    float e = 0.f;
+    const int k = g.k, r = k / 2;
+    for (int i = 0; i < k; ++i) {
+        const int64_t y = h + i - r;
+        const bool yin = y >= 0 && y < g.H;
+        for (int j0 = 0; j0 < k; j0 += 8) {
+            float cv[8], pv[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const int64_t xc = w + j0 + jj - r, xp = d + j0 + jj - r;
+                const bool cin = yin && xc >= 0 && xc < g.W, pin = yin && xp >= 0 && xp < g.W;
+                cv[jj] = ld_bufs<T>(rc, cin ? (uint32_t)((y * g.W + xc) * (int64_t)sizeof(T)) : 0x80000000u, 0u);
+                pv[jj] = ld_bufs<T>(rp, pin ? (uint32_t)((y * g.W + xp) * (int64_t)sizeof(T)) : 0x80000000u, 0u);
+            }
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj)
+                if (j0 + jj < k) e = __builtin_fmaf(cv[jj] - mc, pv[jj] - mp, e);
+        }
+    }
+    const float den = sqrtf(__builtin_fmaf(sc.sq[h * g.W + w], sp.sq[h * g.W + d], kEps));
+    return (e + kEps) / den;
+}
+
 __device__ __forceinline__ int64_t d_of_s(const Geo& g, int64_t w, int64_t s) {
     return g.layout == CUSTMA_LAYOUT_WINDOW ? w + s : s;
 }
@@ -221,7 +255,7 @@ __global__ __launch_bounds__(256) void k_disp_recheck(const T* __restrict__ cam,
         for (int64_t s = threadIdx.x; s < g.DO; s += blockDim.x) {
             const int64_t d = d_of_s(g, w, s);
             if (!voxel_valid(g, w, d)) continue;
-            const float c = exact_cost(cam, proj, g, sc, sp, h, w, d);
+            const float c = exact_cost_batched(cam, proj, g, sc, sp, h, w, d);
             if (so.soft) soft_add(c, (float)s, bv, so.kb, q0, q1);
             amax_merge(bv, bi, c, s);
         }
