@@ -49,14 +49,10 @@ __global__ __launch_bounds__(256) void k_fwd_exact(const T* __restrict__ cam, co
     const int64_t w0 = (int64_t)wt * TWX;
     const int64_t dA = (g.layout == CUSTMA_LAYOUT_WINDOW ? w0 : 0) + (int64_t)dc * TDX;
 
-    for (int e = threadIdx.x; e < k * CW; e += 256) {
-        const int i = e / CW, x = e % CW;
-        camT[e] = ldpad(cam, g.H, g.W, h + i - r, w0 + x - r);
-    }
-    for (int e = threadIdx.x; e < k * PW; e += 256) {
-        const int i = e / PW, x = e % PW;
-        projT[e] = ldpad(proj, g.H, g.W, h + i - r, dA + x - r);
-    }
+    // the patch rows through batched unconditional loads (common.h tile_to_lds; a bounds-tested load
+    // per element was waited for one at a time)
+    tile_to_lds<T, 8>(cam, g.H, g.W, h - r, w0 - r, k, CW, camT, CW, (int)threadIdx.x, 256);
+    tile_to_lds<T, 8>(proj, g.H, g.W, h - r, dA - r, k, PW, projT, PW, (int)threadIdx.x, 256);
     if (threadIdx.x < TWX) {
         const int64_t w = w0 + threadIdx.x;
         const bool ok = w < g.W;
@@ -170,14 +166,10 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_exact_k(const T* __restrict__ c
     const int64_t w0 = (int64_t)wt * TWX;
     const int64_t dA = (g.layout == CUSTMA_LAYOUT_WINDOW ? w0 : 0) + (int64_t)dc * NC;
 
-    for (int e = threadIdx.x; e < KT * CW; e += NTH) {
-        const int i = e / CW, x = e % CW;
-        camT[e] = ldpad(cam, g.H, g.W, h + i - R0, w0 + x - R0);
-    }
-    for (int e = threadIdx.x; e < KT * PW; e += NTH) {
-        const int i = e / PW, x = e % PW;
-        projT[e] = ldpad(proj, g.H, g.W, h + i - R0, dA + x - R0);
-    }
+    // the patch rows through batched unconditional loads (common.h tile_to_lds): a bounds-tested load per
+    // element was waited for one at a time -- ~35 round trips per thread at k = 19, more than the MFMA work
+    tile_to_lds<T, 8>(cam, g.H, g.W, h - R0, w0 - R0, KT, CW, camT, CW, (int)threadIdx.x, NTH);
+    tile_to_lds<T, 8>(proj, g.H, g.W, h - R0, dA - R0, KT, PW, projT, PW, (int)threadIdx.x, NTH);
     if (threadIdx.x < TWX) {
         const int64_t w = w0 + threadIdx.x;
         const bool ok = w < g.W;
