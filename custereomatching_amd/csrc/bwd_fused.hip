@@ -1125,12 +1125,29 @@ __global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict
     float* tB = tZ + L * L;
     const int64_t y0 = (int64_t)blockIdx.y * TS, x0 = (int64_t)blockIdx.x * TS;
     const int Hi = (int)g.H, Wi = (int)g.W;
-    for (int e = threadIdx.x; e < L * L; e += 256) {
-        const int y = (int)y0 + e / L - r, x = (int)x0 + e % L - r;
-        const bool ok = y >= 0 && y < Hi && x >= 0 && x < Wi;
-        const int64_t q = (int64_t)y * Wi + x;
-        tZ[e] = ok ? (float)Zz[q] : 0.f;
-        tB[e] = ok ? (float)Bb[q] : 0.f;
+    // the input tile through unconditional raw buffer loads (outside the image: an out-of-range offset,
+    // read as 0), four items per thread in flight together; a bounds-tested load per item was waited for
+    // one at a time.  Each plane stays below 2 GiB (backward_supported: H W 24 < 2^31).
+    const auto rZ = make_rsrc(Zz, (uint32_t)(plane * 4)), rB = make_rsrc(Bb, (uint32_t)(plane * 4));
+    for (int e0 = 0; e0 < L * L; e0 += 4 * 256) {
+        float z[4], bb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = e0 + (int)threadIdx.x + 256 * i, ee = e < L * L ? e : 0;
+            const int y = (int)y0 + ee / L - r, x = (int)x0 + ee % L - r;
+            const bool ok = e < L * L && y >= 0 && y < Hi && x >= 0 && x < Wi;
+            const uint32_t off = ok ? (uint32_t)(((int64_t)y * Wi + x) * 4) : 0x80000000u;
+            z[i] = ld_bufs<float>(rZ, off, 0u);
+            bb[i] = ld_bufs<float>(rB, off, 0u);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = e0 + (int)threadIdx.x + 256 * i;
+            if (e < L * L) {
+                tZ[e] = z[i];
+                tB[e] = bb[i];
+            }
+        }
     }
     __syncthreads();
     for (int e = threadIdx.x; e < L * TS; e += 256) {
@@ -1147,8 +1164,23 @@ __global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict
     }
     __syncthreads();
     const double sh = (double)shift[side];
-    for (int e = threadIdx.x; e < TS * TS; e += 256) {
-        const int ly = e / TS, lx = e % TS;
+    // the pixels' T1 and image values first, all in flight together (out-of-range offsets past the image)
+    static_assert(TS * TS % 256 == 0, "whole output items per thread");
+    constexpr int NO = TS * TS / 256;
+    const auto rT = make_rsrc(T1, (uint32_t)(plane * 4)), rI = make_rsrc(img, (uint32_t)(plane * sizeof(T)));
+    float tv[NO], iv[NO];
+#pragma unroll
+    for (int j = 0; j < NO; ++j) {
+        const int e = (int)threadIdx.x + 256 * j, ly = e / TS, lx = e % TS;
+        const int64_t y = y0 + ly, x = x0 + lx;
+        const bool ok = y < g.H && x < g.W;
+        const int64_t q = y * g.W + x;
+        tv[j] = ld_bufs<float>(rT, ok ? (uint32_t)(q * 4) : 0x80000000u, 0u);
+        iv[j] = ld_bufs<T>(rI, ok ? (uint32_t)(q * (int64_t)sizeof(T)) : 0x80000000u, 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < NO; ++j) {
+        const int e = (int)threadIdx.x + 256 * j, ly = e / TS, lx = e % TS;
         const int64_t y = y0 + ly, x = x0 + lx;
         if (y >= g.H || x >= g.W) continue;
         double sz = 0, sb = 0;
@@ -1159,8 +1191,8 @@ __global__ __launch_bounds__(256) void k_bwd_combine3(Geo g, const T* __restrict
             sb += hB[f];
         }
         const int64_t q = y * g.W + x;
-        const double ip = (double)to_f(img[q]) - sh;
-        out[q] = (float)((double)T1[q] - sz - ip * sb);
+        const double ip = (double)iv[j] - sh;
+        out[q] = (float)((double)tv[j] - sz - ip * sb);
     }
 }
 
