@@ -437,6 +437,7 @@ int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, 
     if (rows < 0 || n < 0) return fail(CUSTMA_E_ARG, "negative size");
     if (rows == 0) return CUSTMA_OK;
     if (n == 0) return fail(CUSTMA_E_ARG, "argmax over an empty axis");
+    if (n >= ((int64_t)1 << 29)) return fail(CUSTMA_E_UNSUPPORTED, "argmax: a row holds at most 2^29 - 1 values");
     if (!volume || !index) return fail(CUSTMA_E_NULL, "null pointer argument");
     return check_hip(launch_argmax(volume, rows, n, index, best, (hipStream_t)stream), "argmax");
 }
