@@ -155,7 +155,8 @@ int custma_image_u8_to_unit(const uint8_t* image, int64_t H, int64_t W, int32_t 
                             int32_t out_dtype, void* out, void* stream);
 
 /* First-index argmax over the last axis of a [rows, n] fp32 array (torch.argmax semantics), as the
- * reference's callers do on the volume (examples/verify.py:72, examples/test.py:78-83). */
+ * reference's callers do on the volume (examples/verify.py:72, examples/test.py:78-83).  n < 2^29
+ * (CUSTMA_E_UNSUPPORTED otherwise: a row is read through one 32-bit buffer range). */
 int custma_argmax(const float* volume, int64_t rows, int64_t n, int64_t* index, float* best, void* stream);
 
 /* Fused disparity without materialising the volume: index[h][w] = argmax_s cost(h, w, s) (first index
