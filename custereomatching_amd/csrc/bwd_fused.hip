@@ -312,7 +312,12 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         return make_rsrc(a.part + ((size_t)t * a.S + slot) * plane + (size_t)(y0 + yw) * g.W, prow_bytes);
     };
     // loads per issue() (asm_ld2s / asm_ld1s / asm_ld4), per thread
+#ifdef CUSTMA_KO_NOVOL
+    // knock-out (timing only, wrong results): no volume loads, every cost 0.5
+    constexpr int NLD = TRW + (HPW > 0 ? HPW : 1) + (CAML ? 0 : 4);
+#else
     constexpr int NLD = TRW * 2 + (HPW > 0 ? HPW : 1) + (CAML ? 0 : 4);
+#endif
     auto flush = [&](int wfirst, int nsteps) {
         if constexpr (BDP == 2) asm_vmcnt<NLD>();  // all but the newest issue
         int ln = lane;
@@ -420,7 +425,14 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
             const uint32_t sC = (w >= 0 && w < Wi) ? (uint32_t)w * 4u : kWinNR;
             const uint32_t sX = (xb >= 0 && xb < Wi) ? (uint32_t)xb * 4u : kWinNR;
 #pragma unroll
-            for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], vLO[m], vLO[m], dG, dV, sW, sW);
+            for (int m = 0; m < TRW; ++m) {
+#ifdef CUSTMA_KO_NOVOL
+                asm_ld1s<NOP>(b.ge[m], vLO[m], dG, sW);
+                b.cv[m] = 0x3f000000u;
+#else
+                asm_ld2s<NOP>(b.ge[m], b.cv[m], vLO[m], vLO[m], dG, dV, sW, sW);
+#endif
+            }
 #pragma unroll
             for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], vLH[i], dG, sW);
             if constexpr (!CAML) asm_ld4s<NOP>(b.xo, b.xh, b.mc, b.cx, vXo, vXh, vMo, vCo, dPc, sC, sX);
@@ -429,7 +441,14 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
         const bool ve = w >= lwlo && w < lwhi;
         const uint32_t oGe = ve ? (uint32_t)((w * gsU + dl) * 4) : kOOB;
 #pragma unroll
-        for (int m = 0; m < TRW; ++m) asm_ld2s<NOP>(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
+        for (int m = 0; m < TRW; ++m) {
+#ifdef CUSTMA_KO_NOVOL
+            asm_ld1s<NOP>(b.ge[m], oGe, dG, sVo[m]);
+            b.cv[m] = 0x3f000000u;
+#else
+            asm_ld2s<NOP>(b.ge[m], b.cv[m], oGe, oGe, dG, dV, sVo[m], sVo[m]);
+#endif
+        }
 #pragma unroll
         for (int i = 0; i < HP; ++i) asm_ld1s<NOP>(b.hg[i], wv + NWC * i < NH ? oGe : kOOB, dG, sVh[i]);
         if constexpr (!CAML)

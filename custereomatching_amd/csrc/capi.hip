@@ -1,8 +1,8 @@
 // C ABI of libcustma_hip.so (declared in include/custma.h).
 // Validation, workspace carving and dispatch; no allocation, no host
-// synchronisation (graph-capturable).  The one piece of library state is a
-// per-device side stream with two events (created on first use), which an
-// eager large fast forward forks onto and joins back from (forward_split).
+// synchronisation (graph-capturable); every launch of a call goes to the
+// caller's stream.  The only library state is the bench-only event timing
+// (custma_profile_*).
 // Error behaviour: every entry point returns a CUSTMA_E_* code and records a
 // message for custma_last_error(), which the Python shim raises as
 // RuntimeError / ValueError -- unlike the
@@ -69,9 +69,8 @@ int set_band(Geo* g, int64_t row_begin, int64_t row_end) {
     return CUSTMA_OK;
 }
 
-// the two images' statistics, then the fused forward's per-band counters (bands of >= 8 rows)
-size_t stats_bytes(const Geo& g) { return 2 * align256((size_t)g.H * g.W * 20) + align256(4 * (size_t)(g.H / 8 + 1)); }
-int* band_counters(const Geo& g, void* ws) { return (int*)((char*)ws + 2 * align256((size_t)g.H * g.W * 20)); }
+// the two images' statistics
+size_t stats_bytes(const Geo& g) { return 2 * align256((size_t)g.H * g.W * 20); }
 
 size_t volume_bytes(const Geo& g) { return (size_t)g.HV() * g.WO * g.DO * sizeof(float); }
 
@@ -92,68 +91,6 @@ int run_stats(const void* cam, const void* proj, int32_t dtype, const Geo& g, vo
               hipStream_t s, int mode = STATS_FULL, int rows = STATS_ALL_ROWS) {
     carve_stats(g, ws, sc, sp);
     return check_hip(launch_stats(cam, proj, dtype, g, *sc, *sp, s, mode, nullptr, nullptr, rows), "stats");
-}
-
-// The fast window forward of a large band as two halves, so that the second half's statistics pass
-// runs beside the first half's sweep instead of in front of the whole sweep:
-//   s:    stats(A) -> fork -> sweep(A) ........................ wait(join)
-//   side:                    wait(fork) -> stats(B) -> sweep(B) -> join
-// (the halves' statistics and volume rows are disjoint; a half keeps the whole band's row-band
-// height, so the two sweeps launch the same blocks the single sweep would).  Stream order on s is
-// kept: the side stream starts after everything enqueued on s before the call, and s continues
-// after both halves.
-bool split_forward(const Geo& g) {
-    // opt-in (CUSTMA_FWD_SPLIT=1): measured slower than the single-stream form (same-process A/B/C,
-    // profiles/r05/a/ab_split.log: C3 1.030 vs 0.998 ms, C5 9.46 vs 9.35 ms)
-    const char* e = getenv("CUSTMA_FWD_SPLIT");
-    if (!e || e[0] != '1') return false;
-    if (g.layout != CUSTMA_LAYOUT_WINDOW || !disp_tile_ok(g)) return false;
-    const int th = wave_grid(g).TH;
-    return g.HV() >= 8 * th && (double)g.HV() * g.WO * g.DO * 4 >= 1e9;
-}
-
-int forward_split(const void* cam, const void* proj, int32_t dtype, const Geo& g, void* ws, float* out,
-                  hipStream_t s) {
-    SideStream sd;
-    std::unique_lock<std::mutex> lock;
-    int rc = check_hip(side_stream(&sd, &lock), "side stream");
-    if (rc) return rc;
-    SideStream* side = &sd;
-    Geo ga = g, gb = g;
-    ga.band_rows = gb.band_rows = wave_grid(g).TH;
-    const int64_t half = cdiv(cdiv(g.HV(), 2), ga.band_rows) * ga.band_rows;
-    ga.h_hi = gb.h_lo = g.h_lo + half;
-    Stats sc, sp;
-    carve_stats(g, ws, &sc, &sp);
-    if ((rc = check_hip(launch_stats(cam, proj, dtype, ga, sc, sp, s, STATS_FWD, nullptr, nullptr, STATS_BAND_ROWS),
-                        "stats")) ||
-        (rc = check_hip(hipEventRecord(side->fork, s), "fork")))
-        return rc;
-    // from the fork on, the side stream is joined back into s whatever fails below: nothing the
-    // side stream may still write (statistics, volume rows) outlives the caller's stream order
-    if (!(rc = check_hip(launch_fwd_fast(cam, proj, dtype, ga, sc, sp, out, s), "forward(fast)")) &&
-        !(rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "fork wait")) &&
-        !(rc = check_hip(launch_stats(cam, proj, dtype, gb, sc, sp, side->s, STATS_FWD, nullptr, nullptr,
-                                      STATS_BAND_ROWS), "stats")))
-        rc = check_hip(launch_fwd_fast(cam, proj, dtype, gb, sc, sp, out + half * g.WO * g.DO, side->s),
-                       "forward(fast)");
-    const int rj = check_hip(hipEventRecord(side->join, side->s), "join");
-    const int rw = rj ? rj : check_hip(hipStreamWaitEvent(s, side->join, 0), "join wait");
-    return rc ? rc : rw;
-}
-
-// The side stream belongs to the current device; a caller's stream of another device keeps the
-// single-stream form.
-bool stream_on_current_device(hipStream_t s) {
-    int cur = 0;
-    hipDevice_t sd = 0;
-    if (hipGetDevice(&cur) != hipSuccess) return false;
-    if (!s) return true;
-    if (hipStreamGetDevice(s, &sd) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return (int)sd == cur;
 }
 
 int check_dtype(int32_t dtype) {
@@ -208,27 +145,6 @@ size_t bwd_bytes(const Geo& g) {
 // k^2-long fp32 chain by 1.06e-5 (its worst-case bound (k^2 + 6) 2^-24 is 3.8e-5).  Larger k write
 // the exact volume (bit-identical); their fused disparity (certified) and backward still sweep.
 constexpr int kFastVolumeMaxK = 17;
-
-// Side stream of the current device (non-blocking, created once and kept for the process's lifetime,
-// like the runtime's own per-device state), with its fork / join events.
-hipError_t side_stream(SideStream* out, std::unique_lock<std::mutex>* lock) {
-    static std::mutex mu[64];
-    static SideStream ss[64];
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    *lock = std::unique_lock<std::mutex>(mu[dev]);
-    SideStream& x = ss[dev];
-    if (!x.s) {
-        if ((e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&x.join, hipEventDisableTiming)) != hipSuccess ||
-            (e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking)) != hipSuccess)
-            return e;
-    }
-    *out = x;
-    return hipSuccess;
-}
 
 bool fast_supported(int k) {
     switch (k) {
@@ -319,19 +235,6 @@ int custma_forward_band(const void* camera, const void* projector, int32_t dtype
     hipStream_t s = (hipStream_t)stream;
     Stats sc, sp;
     const bool fast = precision == CUSTMA_FAST && fast_supported(g.k) && g.k <= kFastVolumeMaxK;
-    // the statistics pass fused into the sweep's launch (large window volumes)
-    if (fast && fused_forward_ok(g, cost_volume)) {
-        carve_stats(g, workspace, &sc, &sp);
-        return check_hip(launch_fwd_fused(camera, projector, dtype, g, sc, sp, cost_volume, band_counters(g, workspace), s),
-                         "forward(fused)");
-    }
-    // (eager calls only: under stream capture the single-stream form is recorded)
-    if (fast && split_forward(g) && stream_on_current_device(s)) {
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone)
-            return forward_split(camera, projector, dtype, g, workspace, cost_volume, s);
-        (void)hipGetLastError();  // a refused query must not read as a later launch's failure
-    }
     // the fast sweeps read sq and box only; the exact forward reads mean and sq
     // only the volume rows' statistics (a row band's halo rows feed the patches, not the statistics
     // the sweeps read)

@@ -24,7 +24,6 @@ struct Geo {
     int32_t D;
     int64_t WO, DO; // volume [h_hi - h_lo, WO, DO]
     int64_t h_lo, h_hi;  // volume rows = image rows [h_lo, h_hi) (row bands: the rest is halo)
-    int32_t band_rows = 0;  // fast forward sweeps' row-band height (0: wave_grid's choice)
     __host__ __device__ int64_t HV() const { return h_hi - h_lo; }
 };
 
@@ -267,28 +266,21 @@ __device__ __forceinline__ void asm_ld_img4(uint32_t& pe0, uint32_t& pe1, uint32
             : "v"(vP0), "v"(vP1), "s"(dP), "s"(sE), "s"(sL));
     }
 }
-// SC1: the loads bypass this CU's L1 (`sc1`, L2-served): statistics written in the same launch by other
-// workgroups with write-through stores (the fused forward, sweep_wave.hip)
-#define CUSTMA_LD_STAT6(POL)                                                                                  \
-    asm volatile("s_nop 4\n\t"                                                                               \
-                 "buffer_load_dwordx2 %0, %6, %12, %16 offen" POL "\n\t"                                     \
-                 "buffer_load_dwordx2 %1, %7, %12, %16 offen" POL "\n\t"                                     \
-                 "buffer_load_dword %2, %8, %13, %17 offen" POL "\n\t"                                       \
-                 "buffer_load_dword %3, %9, %13, %17 offen" POL "\n\t"                                       \
-                 "buffer_load_dwordx2 %4, %10, %14, %16 offen" POL "\n\t"                                    \
-                 "buffer_load_dword %5, %11, %15, %17 offen" POL                                               \
-                 : "=&v"(m0), "=&v"(m1), "=&v"(q0), "=&v"(q1), "=&v"(ub), "=&v"(uq)                            \
-                 : "v"(vM0), "v"(vM1), "v"(vQ0), "v"(vQ1), "v"(vUB), "v"(vUQ), "s"(dPB), "s"(dPS), "s"(dCB), \
-                   "s"(dCS), "s"(s8), "s"(s4))
-template <bool SC1 = false>
 __device__ __forceinline__ void asm_ld_stat6(double& m0, double& m1, uint32_t& q0, uint32_t& q1, double& ub,
                                              uint32_t& uq, uint32_t vM0, uint32_t vM1, uint32_t vQ0, uint32_t vQ1,
                                              uint32_t vUB, uint32_t vUQ, i32x4 dPB, i32x4 dPS, i32x4 dCB, i32x4 dCS,
                                              uint32_t s8, uint32_t s4) {
-    if constexpr (SC1) CUSTMA_LD_STAT6(" sc1");
-    else CUSTMA_LD_STAT6("");
+    asm volatile("s_nop 4\n\t"
+                 "buffer_load_dwordx2 %0, %6, %12, %16 offen\n\t"
+                 "buffer_load_dwordx2 %1, %7, %12, %16 offen\n\t"
+                 "buffer_load_dword %2, %8, %13, %17 offen\n\t"
+                 "buffer_load_dword %3, %9, %13, %17 offen\n\t"
+                 "buffer_load_dwordx2 %4, %10, %14, %16 offen\n\t"
+                 "buffer_load_dword %5, %11, %15, %17 offen"
+                 : "=&v"(m0), "=&v"(m1), "=&v"(q0), "=&v"(q1), "=&v"(ub), "=&v"(uq)
+                 : "v"(vM0), "v"(vM1), "v"(vQ0), "v"(vQ1), "v"(vUB), "v"(vUQ), "s"(dPB), "s"(dPS), "s"(dCB), "s"(dCS),
+                   "s"(s8), "s"(s4));
 }
-#undef CUSTMA_LD_STAT6
 __device__ __forceinline__ void asm_ld_f64(double& d, uint32_t off, i32x4 r) {
     asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(d) : "v"(off), "s"(r));
 }
@@ -399,17 +391,6 @@ hipError_t launch_u8_to_unit(const uint8_t* src, int64_t npix, int C, int ch, in
 // box (what the fast forward sweeps read).  BAND: only the volume rows [h_lo, h_hi) (a forward or disparity
 // reads the statistics of its volume rows only: voxel (h, w, d) the camera's at (h, w), the projector's at
 // (h, d)); otherwise every image row (the backward reads its gradient rows and their halo).
-// Per-device side stream with fork / join events (capi.hip): the launches that run beside the main
-// stream's work (the split forward, the backward's remainder-diagonal pass) fork onto it after an
-// event on the caller's stream and join back before anything that reads their results.
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-// The current device's side stream; `lock` guards a fork ... join enqueue sequence (the events are
-// shared, and a wait binds to the most recent record at the time it is enqueued).
-hipError_t side_stream(SideStream* out, std::unique_lock<std::mutex>* lock);
-
 enum StatsMode {
     STATS_FULL = CUSTMA_STATS_FULL,
     STATS_BOX = CUSTMA_STATS_BOX,

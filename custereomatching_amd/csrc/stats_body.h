@@ -38,15 +38,12 @@ __host__ __device__ constexpr int lx_for(int k) {
 //   STATS_MSB       mean, sq, box             (the disparity: its sweep reads sq, box, the exact
 //                                              recheck mean, sq; the exact forward: mean, sq)
 // One statistics tile (TX x TY pixels of image bz, tile (tbx, tby) of the row range [ybeg, yend)) by the 256
-// threads of a workgroup; `lds_d` = the dynamic LDS of stats_lds_bytes().  SC1: every output stored
-// write-through (`sc1`, agent scope) -- the fused forward (sweep_wave.hip k_fwd_tile<..., FUSED>) reads the
-// statistics in the same launch, on other CUs, with `sc1` loads after a per-band counter.
-template <bool SC1, typename V>
+// threads of a workgroup; `lds_d` = the dynamic LDS of stats_lds_bytes().
+template <typename V>
 __device__ __forceinline__ void stats_put(V* p, V v) {
-    if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
+    *p = v;
 }
-template <typename T, int KT, int MODE, bool SC1 = false>
+template <typename T, int KT, int MODE>
 __device__ __forceinline__ void stats_tile(const T* __restrict__ img0, const T* __restrict__ img1, const Geo& g,
                                            const Stats& st0, const Stats& st1, float* __restrict__ prep,
                                            const float* __restrict__ shift, int64_t ybeg, int64_t yend, int tbx,
@@ -188,18 +185,18 @@ __device__ __forceinline__ void stats_tile(const T* __restrict__ img0, const T* 
                 if (x >= g.W) break;
                 const double b = bx[p][c];
                 const int64_t o = y * g.W + x;
-                stats_put<SC1>(st.box + o, b);
+                stats_put(st.box + o, b);
                 const double c2 = b2[p][c] - b * b / (double)(k * k);
                 const float sqt = (float)(c2 > 0.0 ? c2 : 0.0);
                 if constexpr (MODE == STATS_BWD_PREP) {
                     const int64_t n = g.H * g.W;
                     float* pz = prep + 3 * n * bz;
-                    stats_put<SC1>(pz + o, sqt);
-                    stats_put<SC1>(pz + n + o, (float)(b / (double)(k * k) - (double)shift[bz]));
+                    stats_put(pz + o, sqt);
+                    stats_put(pz + n + o, (float)(b / (double)(k * k) - (double)shift[bz]));
                     // raw: the sweep subtracts the shift after a zero-padded load
-                    stats_put<SC1>(pz + 2 * n + o, tile[(ly0 + p + r0) * LX + lx0 + c + r0]);
+                    stats_put(pz + 2 * n + o, tile[(ly0 + p + r0) * LX + lx0 + c + r0]);
                 } else {
-                    stats_put<SC1>(st.sqt + o, sqt);
+                    stats_put(st.sqt + o, sqt);
                 }
             }
         }
@@ -303,7 +300,7 @@ __device__ __forceinline__ void stats_tile(const T* __restrict__ img0, const T* 
         const int64_t xp = x0 + lx0, op = y * g.W + xp;
         const bool al = (((uintptr_t)(st.sq + op) | (uintptr_t)(st.mean + op) | (uintptr_t)(st.sqt + op)) & 7) == 0 &&
                         ((uintptr_t)(st.box + op) & 15) == 0;
-        if (!SC1 && (g.W & 1) == 0 && xp + 1 < g.W && al) {
+        if ((g.W & 1) == 0 && xp + 1 < g.W && al) {
             static_assert(PC == 2, "column pairs");
             if constexpr (MODE == STATS_FULL || MODE == STATS_MSB) *(f32x2*)(st.mean + op) = f32x2{m[p][0], m[p][1]};
             *(f32x2*)(st.sq + op) = f32x2{sq[p][0], sq[p][1]};
@@ -325,12 +322,12 @@ __device__ __forceinline__ void stats_tile(const T* __restrict__ img0, const T* 
             if (x >= g.W) break;
             const int64_t o = y * g.W + x;
             const double b = bx[p][c];
-            if constexpr (MODE == STATS_FULL || MODE == STATS_MSB) stats_put<SC1>(st.mean + o, m[p][c]);
-            stats_put<SC1>(st.sq + o, sq[p][c]);
-            stats_put<SC1>(st.box + o, b);
+            if constexpr (MODE == STATS_FULL || MODE == STATS_MSB) stats_put(st.mean + o, m[p][c]);
+            stats_put(st.sq + o, sq[p][c]);
+            stats_put(st.box + o, b);
             if constexpr (MODE == STATS_FULL) {
                 const double c2 = b2[p][c] - b * b / (double)(k * k);
-                stats_put<SC1>(st.sqt + o, (float)(c2 > 0.0 ? c2 : 0.0));
+                stats_put(st.sqt + o, (float)(c2 > 0.0 ? c2 : 0.0));
             }
         }
     }

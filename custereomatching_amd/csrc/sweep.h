@@ -206,15 +206,6 @@ template <int K>
 hipError_t sw_fwd(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, float* out,
                   hipStream_t s);
 template <int K>
-hipError_t sw_fwd_fused(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, float* out,
-                        int* cnt, hipStream_t s);
-// The fast window forward with its statistics pass fused into the sweep's launch (sweep_wave.hip
-// k_fwd_tile FUSED): window layout, four diagonal chunks, 64-row bands, W % 32 == 0, 16-byte aligned
-// volume blocks, >= 8 bands (one per XCD).  cnt: nBand ints of workspace (zeroed by the launch).
-bool fused_forward_ok(const Geo& g, const void* out);
-hipError_t launch_fwd_fused(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
-                            float* out, int* cnt, hipStream_t s);
-template <int K>
 hipError_t sw_amx(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, DispPartial part,
                   hipStream_t s);
 

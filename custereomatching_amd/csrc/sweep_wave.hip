@@ -29,7 +29,6 @@
 #include <type_traits>
 
 #include "common.h"
-#include "stats_body.h"
 #include "sweep.h"
 
 // Build: compiled once per kernel size with -DCUSTMA_SW_K=<k> (the kernels and launchers of
@@ -78,7 +77,7 @@ constexpr int kFwdPF = 2;  // outputs whose projector statistics are read ahead 
 // scan's 16 lanes (the columns past DO padded with -FLT_MAX)
 constexpr int kAmxPitch = 16 * ((64 * kTileMaxChunks + 1 + 15) / 16);
 template <int K, typename T, bool FULL_EDGE, bool REM, bool STAGED = false, int SS = TW, int P = 2, int AMX_ = 0,
-          bool CPL = false, bool SC1 = false>
+          bool CPL = false>
 __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __restrict__ proj, const Geo& g,
                                           const Stats& sc, const Stats& sp, float* __restrict__ out,
                                           int64_t u0, int64_t h0, int64_t h1, int64_t d0,
@@ -164,7 +163,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
             if constexpr (C3R) asm_ld_img2<T>(p.ce2, p.cl2, vC2, dCam, sE, sL);
         }
         const bool st = ti >= h0i && ti < h1i;
-        asm_ld_stat6<SC1>(p.m0, p.m1, p.q0, p.q1, p.ub, p.uq, vM0, vM1, vQ0, vQ1, vUB, vUQ, dPB, dPS, dCB, dCS,
+        asm_ld_stat6(p.m0, p.m1, p.q0, p.q1, p.ub, p.uq, vM0, vM1, vQ0, vQ1, vUB, vUQ, dPB, dPS, dCB, dCS,
                      so_row(ti, rb8, st), so_row(ti, rb4, st));
     };
     auto tie = [&](Stage& p) {
@@ -201,8 +200,12 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
     // issues, so a peeled prologue with another register assignment would be joined to the
     // loop by register copies -- reads of registers whose loads are still in flight.
     Stage st[P];
-    // stores per step (every thread issues exactly ST: the hand-counted waits rely on it)
-    constexpr int ST = AMX > 0 ? (SOFT ? 5 : 3) * AMX : STAGED ? (SS < 0 ? 1 - SS : SS) : TW + (REM ? 1 : 0);
+    // stores per step (every thread issues exactly ST: the hand-counted waits rely on it).  Each store
+    // site below restates its own count in a static_assert (ST_*), so a site whose store count changes
+    // without ST fails to compile; every store there is unconditional (masked by an out-of-range
+    // offset, never by a branch), so the count is the same for every thread and step.
+    constexpr int ST_AMX = (SOFT ? 5 : 3) * AMX, ST_X4 = -SS + 1, ST_DW = SS, ST_DIRECT = TW + (REM ? 1 : 0);
+    constexpr int ST = AMX > 0 ? ST_AMX : STAGED ? (SS < 0 ? ST_X4 : ST_DW) : ST_DIRECT;
     static_assert((P - 1) * (kLoads + ST) <= 63, "vmcnt holds the pipeline");
     // out_c: std::true_type for an output step (t >= h0: stores), std::false_type for a warm-up step
     // (P == 2: both fixed at compile time, so the waits are too); a runtime bool with P == 3
@@ -354,9 +357,11 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                 }
                 if constexpr (STAGED) {
                     if (!MASKED || dv) sb[m * SPc + d0 + l] = c;
-                } else
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, so,
+                } else {
+                    static_assert(STAGED || ST == TW + (REM ? 1 : 0), "ST_DIRECT: one store per tile row (+ REM's)");
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, c), rOut, vo, so,
                                                       kStoreAux);
+                }
             });
             };
             if (!STAGED || allv) outputs(std::false_type{});
@@ -401,6 +406,8 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                     const auto rQ0 = make_rsrc(soft ? part.s0 + prow : part.best, soft ? pb : 0u);
                     const auto rQ1 = make_rsrc(soft ? part.s1 + prow : part.best, soft ? pb : 0u);
                     const float kb = part.kb;
+                    // AMX passes x (best, second, index [, s0, s1]) stores
+                    static_assert(ST == AMX * (3 + (SOFT ? 2 : 0)), "ST_AMX");
 #pragma unroll
                     for (int ps = 0; ps < AMX; ++ps) {
                         const int m = (ps * nw + wv) * 4 + (l >> 4);  // tile row of this 16-lane group
@@ -451,6 +458,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                         }
                     }
                 } else if constexpr (SS < 0) {  // block base 16-byte aligned (checked at launch)
+                    static_assert(ST == -SS + 1, "ST_X4: -SS 16-byte stores + the tail's dword store");
                     const int n4 = total >> 2;
                     typedef __attribute__((address_space(3))) volatile i32x4 lds_v4;
 #pragma unroll
@@ -466,6 +474,7 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                                                           (tid < 4 && j < total) ? (uint32_t)(j * 4) : OOB, 0u,
                                                           kStoreAux);
                 } else {
+                    static_assert(ST == SS, "ST_DW: SS dword stores");
 #pragma unroll
                     for (int i = 0; i < SS; ++i) {
                         const int idx = i * NT + tid;
@@ -570,91 +579,15 @@ __global__ __launch_bounds__(64) void k_fwd_wave(const T* __restrict__ cam, cons
 constexpr int kTileP = 2;  // load pipeline depth (steps; 3 measured no faster)
 constexpr int kWaveLds = (3 * kRowP + 64) * 8 + kRowP * 4;  // rowE, rowL, sM, sR (f64) + sQ (f32)
 
-// FUSED (the statistics pass in the same launch; window layout, four chunks, 64-row bands): a
-// workgroup is either a STATISTICS tile (stats_body.h: 32 columns x 64 rows of one image, mode
-// STATS_FWD, stored write-through) or a SWEEP tile.  Each XCD (hardware block b runs on XCD b % 8,
-// the observed round-robin) walks its own contiguous range of bands in the order
-//     S(b0) S(b1) [T(b0) S(b2)] [T(b1) S(b3)] ... T(b_last)
-// (S(b): the band's nSC x 2 statistics tiles, T(b): its nTile sweep tiles), so the statistics of band
-// b + 2 run beside the sweeps of band b instead of as a separate pass in front of the whole sweep.
-// A statistics tile counts itself into cnt[band] (agent-scope atomic add after every storing wave's
-// `s_waitcnt vmcnt(0)` and a barrier); a sweep tile's first lane polls cnt[band] (`sc1` load) until
-// all of the band's tiles have counted, and the sweep reads the statistics with `sc1` loads (L1
-// bypassed, served by L2 / memory; the rows are whole 128-byte lines, W % 32 == 0).  A sweep tile
-// waits only for tiles of LOWER hardware index, so the grid cannot deadlock whatever the placement
-// (blocks start in index order); the poll is bounded, never a hang.
-constexpr int kFusedMinK = 3;
-// CUSTMA_FWD_FUSED=2: the sweep tiles take one agent-scope acquire after their poll and read the
-// statistics with plain loads (=1: `sc1` loads, no acquire)
-inline bool fused_acquire() {
-    const char* e = getenv("CUSTMA_FWD_FUSED");
-    return e && e[0] == '2';
-}
-struct FusedGrid {
-    int nBand, nTile, nSC, P, perX, len;  // P = 2 nSC statistics tiles per band; perX bands per XCD
-};
-
-template <int K, typename T, bool X4, int AMX = 0, bool CPL = false, bool FUSED = false, bool FUSED_ACQ = false>
+template <int K, typename T, bool X4, int AMX = 0, bool CPL = false>
 __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __restrict__ cam,
                                                                  const T* __restrict__ proj, Geo g, Stats sc,
                                                                  Stats sp, float* __restrict__ out, WaveGrid wg,
-                                                                 DispPartial part, int* cnt = nullptr,
-                                                                 FusedGrid fg = FusedGrid{}) {
+                                                                 DispPartial part) {
     extern __shared__ __attribute__((aligned(16))) double lds_t[];
     const int w = (int)(threadIdx.x >> 6);
-    int wt, band;
-    if constexpr (FUSED) {
-        const int x = (int)(blockIdx.x % 8), j0 = (int)(blockIdx.x / 8);
-        const int blo = x * fg.perX, m = min(fg.perX, fg.nBand - blo);
-        if (m <= 0) return;
-        int j = j0, sb = -1, si = 0;
-        wt = -1;
-        band = 0;
-        const int pre = min(2, m) * fg.P;
-        if (j < pre) {
-            sb = blo + j / fg.P;
-            si = j % fg.P;
-        } else {
-            j -= pre;
-            const int G = fg.nTile + fg.P, full = max(0, m - 2);
-            if (j < full * G) {
-                const int gi = j / G, r = j % G;
-                if (r < fg.nTile) { band = blo + gi; wt = r; }
-                else { sb = blo + gi + 2; si = r - fg.nTile; }
-            } else {
-                j -= full * G;
-                const int gi = full + j / fg.nTile;
-                if (gi >= m) return;
-                band = blo + gi;
-                wt = j % fg.nTile;
-            }
-        }
-        if (sb >= 0) {  // statistics tile: image si / nSC, column tile si % nSC, row tile sb
-            stats_detail::stats_tile<T, K, STATS_FWD, true>(cam, proj, g, sc, sp, nullptr, nullptr, g.h_lo, g.h_hi,
-                                                           si % fg.nSC, sb, si / fg.nSC, lds_t);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores are out
-            __syncthreads();
-            if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + sb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        if (threadIdx.x == 0) {  // wait for the band's statistics (bounded: ~0.2 s, then go on)
-            for (int it = 0; it < (1 << 20); ++it) {
-                if (__hip_atomic_load(cnt + band, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= fg.P) break;
-                __builtin_amdgcn_s_sleep(8);
-            }
-            // FUSED_ACQ: one agent-scope acquire (this CU's L1 invalidated), then the statistics are read
-            // with plain loads; else every statistics load is an `sc1` load
-            if constexpr (FUSED_ACQ) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-        __syncthreads();
-    } else {
-        const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
-        wt = (int)(bid % wg.nTile);
-        band = (int)(bid / wg.nTile);
-    }
+    const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int wt = (int)(bid % wg.nTile), band = (int)(bid / wg.nTile);
     char* mine = (char*)lds_t + w * kWaveLds;
     double* rowE = (double*)mine;
     double* rowL = rowE + kRowP;
@@ -675,13 +608,13 @@ __global__ __launch_bounds__(64 * kTileMaxChunks) void k_fwd_tile(const T* __res
     constexpr int S0 = X4 ? -4 : TW, S1 = X4 ? -5 : TW + 1;
     constexpr int kTP = X4 ? kTileP : 2;  // deeper pipelines only with the 16-byte stores (vmcnt range)
     if (!wg.rem)
-        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, false, true, S0, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                          rowL, sM, sQ, sR, stage, part, camL);
     else if (w == wg.nChunk - 1)
-        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, true, true, S1, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                         rowL, sM, sQ, sR, stage, part, camL);
     else
-        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL, FUSED && !FUSED_ACQ>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
+        wave_body<K, T, false, false, true, S1, kTP, AMX, CPL>(cam, proj, g, sc, sp, out, u0, h0, h1, d0, rowE,
                                                                          rowL, sM, sQ, sR, stage, part, camL);
 }
 
@@ -732,53 +665,6 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
     return hipGetLastError();
 }
 
-// The fused forward (statistics + sweep in one launch, FusedGrid; the caller checked fused_forward_ok()):
-// cnt (nBand ints of workspace) is zeroed on the stream before the launch.
-template <int K, typename T>
-hipError_t launch_fused(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, float* out, int* cnt,
-                        hipStream_t s) {
-    if constexpr (K < kFusedMinK) {  // (the statistics body at k <= 2 keeps a small array in scratch)
-        return hipErrorInvalidValue;
-    } else {
-    const WaveGrid wg = wave_grid(g);
-    if (wg.nChunk != kTileMaxChunks || wg.TH != 64) return hipErrorInvalidValue;
-    FusedGrid fg;
-    fg.nBand = wg.nBand;
-    fg.nTile = wg.nTile;
-    fg.nSC = (int)cdiv(g.W, 32);
-    fg.P = 2 * fg.nSC;
-    fg.perX = (int)cdiv(wg.nBand, 8);
-    const int m = fg.perX;  // the longest per-XCD sequence (XCD 0 holds perX bands)
-    fg.len = min(2, m) * fg.P + max(0, m - 2) * (fg.nTile + fg.P) + min(2, m) * fg.nTile;
-    size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)g.DO * 4;
-    const bool cpl = cpl_ok<K, T>(g, wg, lds);
-    if (cpl) lds += cpl_bytes<K, T>(wg);
-    lds = std::max(lds, stats_detail::stats_lds_bytes(STATS_FWD, K));
-    hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)fg.nBand, s);
-    if (e != hipSuccess) return e;
-    const dim3 grid((unsigned)(8 * (int64_t)fg.len)), blk(64 * wg.nChunk);
-    prof_begin(PROF_FWD, s);
-    auto go = [&](auto cpl_, auto acq_) -> hipError_t {
-        constexpr bool CPLV = decltype(cpl_)::value, ACQ = decltype(acq_)::value;
-        hipError_t r = allow_lds(k_fwd_tile<K, T, true, 0, CPLV, true, ACQ>, lds);
-        if (r != hipSuccess) return r;
-        hipLaunchKernelGGL((k_fwd_tile<K, T, true, 0, CPLV, true, ACQ>), grid, blk, lds, s, cam, proj, g, sc, sp, out,
-                           wg, DispPartial{}, cnt, fg);
-        return hipSuccess;
-    };
-    const bool acq = fused_acquire();
-    if (cpl) {
-        if constexpr (sizeof(T) == 2)
-            e = acq ? go(std::true_type{}, std::true_type{}) : go(std::true_type{}, std::false_type{});
-    } else {
-        e = acq ? go(std::false_type{}, std::true_type{}) : go(std::false_type{}, std::false_type{});
-    }
-    if (e != hipSuccess) return e;
-    prof_end(PROF_FWD, s);
-    return hipGetLastError();
-    }
-}
-
 // Fused disparity through the tile kernel (window layout, D + 1 <= 257): one partial per pixel.
 template <int K, typename T>
 hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, DispPartial part, hipStream_t s) {
@@ -809,13 +695,6 @@ hipError_t sw_fwd(const void* cam, const void* proj, int dtype, const Geo& g, St
     return launch_k<K, float>((const float*)cam, (const float*)proj, g, sc, sp, out, s);
 }
 template <int K>
-hipError_t sw_fwd_fused(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, float* out,
-                        int* cnt, hipStream_t s) {
-    if (dtype == CUSTMA_F16)
-        return launch_fused<K, __half>((const __half*)cam, (const __half*)proj, g, sc, sp, out, cnt, s);
-    return launch_fused<K, float>((const float*)cam, (const float*)proj, g, sc, sp, out, cnt, s);
-}
-template <int K>
 hipError_t sw_amx(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp, DispPartial part,
                   hipStream_t s) {
     if (dtype == CUSTMA_F16) return launch_amx<K, __half>((const __half*)cam, (const __half*)proj, g, sc, sp, part, s);
@@ -823,8 +702,6 @@ hipError_t sw_amx(const void* cam, const void* proj, int dtype, const Geo& g, St
 }
 #ifdef CUSTMA_SW_K
 template hipError_t sw_fwd<CUSTMA_SW_K>(const void*, const void*, int, const Geo&, Stats, Stats, float*, hipStream_t);
-template hipError_t sw_fwd_fused<CUSTMA_SW_K>(const void*, const void*, int, const Geo&, Stats, Stats, float*, int*,
-                                              hipStream_t);
 template hipError_t sw_amx<CUSTMA_SW_K>(const void*, const void*, int, const Geo&, Stats, Stats, DispPartial,
                                         hipStream_t);
 #endif
@@ -844,7 +721,6 @@ WaveGrid wave_grid(const Geo& g) {
     wg.TH = 64;  // band height (32 / 128 measured within 2 %)
     // keep >= ~8 waves per SIMD on small problems
     while (wg.TH > 8 && (int64_t)wg.nTile * wg.nChunk * cdiv(g.HV(), wg.TH) < 8192) wg.TH /= 2;
-    if (g.band_rows > 0) wg.TH = g.band_rows;  // a part of a split forward keeps the whole band's height
     wg.nBand = (int)cdiv(g.HV(), wg.TH);
     return wg;
 }
@@ -858,28 +734,6 @@ hipError_t launch_disp_tile(const void* cam, const void* proj, int dtype, const 
     switch (g.k) {
 #define CUSTMA_K(KK) \
     case KK: return sw_amx<KK>(cam, proj, dtype, g, sc, sp, part, s);
-        CUSTMA_SWEEP_KS(CUSTMA_K)
-#undef CUSTMA_K
-        default: return hipErrorInvalidValue;
-    }
-}
-
-bool fused_forward_ok(const Geo& g, const void* out) {
-    // opt-in (CUSTMA_FWD_FUSED=1): measured slower than the separate statistics pass + one sweep
-    // (same-process A/B/C, profiles/r05/a/ab_split.log: C3 1.030 vs 0.998 ms, C5 9.56 vs 9.35 ms)
-    const char* e = getenv("CUSTMA_FWD_FUSED");
-    if (!e || (e[0] != '1' && e[0] != '2')) return false;
-    if (g.layout != CUSTMA_LAYOUT_WINDOW || g.W % 32 != 0 || g.band_rows > 0 || g.k < 3) return false;
-    const WaveGrid wg = wave_grid(g);
-    const bool x4 = ((uintptr_t)out % 16 == 0) && (g.WO % 4 == 0 || g.DO % 4 == 0);
-    return x4 && wg.nChunk == kTileMaxChunks && wg.TH == 64 && wg.nBand >= 8;  // every XCD holds a band
-}
-
-hipError_t launch_fwd_fused(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
-                            float* out, int* cnt, hipStream_t s) {
-    switch (g.k) {
-#define CUSTMA_K(KK) \
-    case KK: return sw_fwd_fused<KK>(cam, proj, dtype, g, sc, sp, out, cnt, s);
         CUSTMA_SWEEP_KS(CUSTMA_K)
 #undef CUSTMA_K
         default: return hipErrorInvalidValue;

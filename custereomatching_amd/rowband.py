@@ -335,10 +335,15 @@ def _group_for(rbg, kernel_size, group, n, H, device):
     if rbg is None:
         if H is None:
             return RowBandGroup(kernel_size, group, n=n, H=H, device=device)
-        key = (id(group), kernel_size, int(n), int(H), str(device))
+        # keyed on the resolved group object and this rank's place in it: after destroy_process_group()
+        # and a re-init, WORLD is a new object (and rank / size may differ), so a RowBandGroup built for
+        # the old group is never reused
+        pg = dist.group.WORLD if group is None else group
+        key = (id(pg), dist.get_rank(pg), dist.get_world_size(pg), kernel_size, int(n), int(H), str(device))
         hit = _GROUPS.get(key)
-        if hit is None or hit.group is not group:
+        if hit is None or hit.pg is not pg:
             hit = RowBandGroup(kernel_size, group, n=n, H=H, device=device)
+            hit.pg = pg
             if len(_GROUPS) >= 64:
                 _GROUPS.clear()
             _GROUPS[key] = hit

@@ -12,12 +12,9 @@
  * pre-zeroing needed).  `workspace` is device memory of at least
  * custma_workspace_bytes(...) bytes, owned by the caller (the torch caching
  * allocator in the Python shim); no device memory is allocated inside a call
- * and nothing synchronises the host.  Work runs on `stream`, except that an
- * eager (not capturing) fast window forward of >= 1 GB that does not take the
- * fused form (statistics tiles inside the sweep's launch) forks its second half
- * onto a per-device side stream the library creates once, and makes `stream`
- * wait for it before returning (stream order is unchanged).  Under capture
- * every call stays on `stream`, so every call is hipGraph-capturable
+ * and nothing synchronises the host.  Every launch of a call goes to
+ * `stream` (no side streams, no library-owned streams or events), so every
+ * call is hipGraph-capturable
  * (tests/test_gpu_graph.py captures forward + backward into a
  * torch.cuda.CUDAGraph and replays it bit-identically).
  */

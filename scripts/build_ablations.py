@@ -13,6 +13,9 @@ BWD = ["bwd_fused.hip"]
 VARIANTS = {
     # backward loads two steps ahead (profiles/r04/a/bwd_depth_ab.txt)
     "bdp2": (["CUSTMA_BWD_DEPTH=2"], BWD),
+    # knock-out (timing only, wrong results): k_bwd_coop without its volume loads -- the most an in-sweep
+    # recompute of the costs could save
+    "ko_novol": (["CUSTMA_KO_NOVOL"], BWD),
     # statistics tile: 32 x 32 pixels, 4 rows per thread is the default (profiles/r03/stats)
     "stats32x8": (["CUSTMA_STATS_TX=32", "CUSTMA_STATS_PR=8"], ["stats.hip"]),
     "stats16x8": (["CUSTMA_STATS_TX=16", "CUSTMA_STATS_PR=8"], ["stats.hip"]),

@@ -55,6 +55,34 @@ __global__ __launch_bounds__(256) void k_tile(float* out, int64_t H, int64_t WO,
         if (BAR) __syncthreads();
     }
 }
+// Persistent form (round 6): G workgroups, workgroup j writes the global tile-rows [j R / G, (j + 1) R / G)
+// of the tile-major order q = wt H + h (R = nTile H): every workgroup the same number of steps (+-1), so no
+// last partial round of workgroups; a range crossing a tile boundary continues in the next tile.
+template <int TW>
+__global__ __launch_bounds__(256) void k_ptile(float* out, int64_t H, int64_t WO, int64_t DO, int nTile) {
+    extern __shared__ float pad[];
+    if (threadIdx.x == 1000) pad[0] = 0.f;
+    const int64_t R = (int64_t)nTile * H, j = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t q0 = j * R / gridDim.x, q1 = (j + 1) * R / gridDim.x;
+    const int tid = threadIdx.x;
+    for (int64_t q = q0; q < q1; ++q) {
+        const int64_t wt = q / H, t = q % H, u0 = wt * TW;
+        const int nrow = (int)min((int64_t)TW, WO - u0);
+        const int total = nrow * (int)DO;
+        float* blk = out + (t * WO + u0) * DO;
+        const auto r = rsrc(blk, (uint32_t)(total * 4));
+        const int n4 = total >> 2;
+        for (int jj = tid; jj < n4 + 1; jj += 256) {
+            if (jj < n4) {
+                const i32x4 v = {jj, jj, jj, (int)t};
+                __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)(jj * 16), 0u, 2);
+            } else if (tid < 256) {
+                for (int e = 4 * n4; e < total; ++e) blk[e] = 1.f;
+            }
+        }
+        __syncthreads();
+    }
+}
 template <int AUX>
 __global__ void k_dword(float* out, int64_t n) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -129,5 +157,12 @@ int main() {
     TILE(true, 2, true, 1, 32, 64, 50000, "x4 nt bar");
     TILE(true, 2, true, 1, 16, 128, 50000, "x4 nt bar");
     TILE(true, 2, true, 1, 16, 32, 50000, "x4 nt bar");
+    {
+        const int nTile = (int)((WO + 15) / 16);
+        for (int G : {768, 1536, 2304}) {
+            snprintf(nm, sizeof nm, "ptile16 persistent G%d lds48K x4 nt bar", G);
+            time(nm, [&] { hipLaunchKernelGGL(k_ptile<16>, dim3(G), dim3(256), 50000, 0, out, H, WO, DO, nTile); });
+        }
+    }
     return 0;
 }

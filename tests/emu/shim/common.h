@@ -20,10 +20,6 @@
 #define __forceinline__ inline
 #define __launch_bounds__(...)
 #define __shared__
-// stats_body.h's SC1 form (agent-scope __hip_atomic_store, a clang builtin) is not instantiated here
-#ifndef __HIP_MEMORY_SCOPE_AGENT
-#define __HIP_MEMORY_SCOPE_AGENT 3
-#endif
 
 struct dim3 {
     unsigned x, y, z;

@@ -1,0 +1,95 @@
+"""Parity hardening of the default fast volume where its worst-case bound passes 1e-5.
+
+The fast sweep's numerator is exact (fp64 sliding sums of exact products); it differs from the reference only
+by the reference's own fp32 rounding, bounded by (k^2 + 6) 2^-24 -- which exceeds north_star's 1e-5 from
+k = 13 on.  `capi.hip` keeps the fast volume up to kFastVolumeMaxK = 17 because the measured difference stays
+far below the bound.  These tests measure it at 256 x 512 (both layouts) on the inputs where fp32 chains
+round worst: quantized-smooth images (verify.py:138-139's preprocessing), large flat regions, and a constant
+plus 1e-4 noise.  The reference arithmetic at full size is the exact forward (bit-identical to the C oracle:
+tests/test_gpu_parity.py::test_exact_forward_bit_identical, re-anchored here on an oracle band).
+
+Also the drop-in argmax story (verify.py:72): torch.max over the `exact` volume is the oracle's argmax bit for
+bit; over the default `fast` volume it agrees wherever the top-2 gap exceeds twice the fast bound (the
+certified path for a bit-exact disparity map is `stereo_disparity`).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.golden.inputs import make_pair
+
+import custereomatching_amd as cm
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _dev(x, dev, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev).to(dtype)
+
+
+def _ill_pair(H, W, D, kind):
+    """Camera = projector shifted by a per-row disparity (as tests/golden/inputs.py), on ill-conditioned
+    images."""
+    rng = np.random.default_rng(11)
+    if kind == "quantized":
+        return make_pair(H, W, D, seed=11, kind="quantized")
+    if kind == "flat":
+        # 32 x 32 constant blocks of 8-bit levels with a few textured islands
+        lv = np.round(rng.uniform(0, 1, (H // 32 + 1, (W + D) // 32 + 2)) * 255) / 255
+        proj = np.kron(lv, np.ones((32, 32)))[:H, :W + D]
+        isl = rng.uniform(0, 1, proj.shape) < 0.002
+        proj = np.where(isl, np.round(rng.uniform(0, 1, proj.shape) * 255) / 255, proj)
+    elif kind == "const_eps":
+        proj = 0.5 + 1e-4 * rng.standard_normal((H, W + D))
+    else:
+        raise ValueError(kind)
+    proj = proj.astype(np.float32)
+    disp = rng.integers(0, max(D, 1), size=H)
+    cam = np.stack([proj[h, disp[h]:disp[h] + W] for h in range(H)])
+    return np.ascontiguousarray(cam, dtype=np.float32), np.ascontiguousarray(proj[:, :W])
+
+
+@pytest.mark.parametrize("layout,D", [("window", 64), ("full", 0)])
+@pytest.mark.parametrize("kind", ["quantized", "flat", "const_eps"])
+@pytest.mark.parametrize("k", [13, 15, 17])
+def test_fast_volume_within_1e5_at_k13_to_17(gpu, k, kind, layout, D):
+    H, W = 256, 512
+    cam, proj = _ill_pair(H, W, max(D, 16), kind)
+    c, p = _dev(cam, gpu), _dev(proj, gpu)
+    ex = cm.cost_volume_forward(c, p, D, k, layout, "exact")
+    fa = cm.cost_volume_forward(c, p, D, k, layout, "fast")
+    # the reference arithmetic at full size: the exact volume, anchored to the C oracle on a band of rows
+    h0, h1 = 120, 124
+    o, a = k // 2, k - 1 - k // 2
+    lay, Dl = (O.FULL, 0) if layout == "full" else (O.WINDOW, D)
+    ref = O.forward(cam[h0 - o:h1 + a], proj[h0 - o:h1 + a], k, layout=lay, D=Dl)[o:o + h1 - h0]
+    assert np.array_equal(ex[h0:h1].cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    err = float((fa - ex).abs().max())
+    assert err <= 1e-5, f"fast volume {err:.3g} from the reference arithmetic (k = {k}, {kind}, {layout})"
+
+
+@pytest.mark.parametrize("kind", ["textured", "quantized"])
+def test_exact_volume_torch_max_is_reference_argmax(gpu, kind):
+    """configs[0] through the reference driver's own selection (verify.py:72: torch.max over the flattened
+    volume): with precision="exact" the index map is the oracle's argmax bit for bit; with the default fast
+    volume it is so wherever the oracle's top-2 gap exceeds twice the fast bound (tie-margin exact)."""
+    z = np.load(os.path.join(GOLD, f"verify_{kind}_128x256_k5.npz"))
+    cam, proj, k = z["cam"], z["proj"], int(z["k"])
+    H, W = cam.shape
+    c, p = _dev(cam, gpu), _dev(proj, gpu)
+    ref = O.forward(cam, proj, k, layout=O.FULL, D=0)
+    ridx = ref.reshape(H * W, -1).argmax(-1)
+    ex = cm.cost_volume_forward(c, p, 0, k, "full", "exact")
+    mx, idx = torch.max(ex.detach().contiguous().reshape(H * W, -1), dim=-1)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    assert np.array_equal(mx.cpu().numpy().view(np.uint32), ref.reshape(H * W, -1).max(-1).view(np.uint32))
+    fa = cm.cost_volume_forward(c, p, 0, k, "full", "fast")
+    _, fidx = torch.max(fa.reshape(H * W, -1), dim=-1)
+    srt = np.sort(ref.reshape(H * W, -1), axis=-1)
+    sure = (srt[:, -1] - srt[:, -2]) > 2 * O.fast_tolerance(k)
+    assert np.array_equal(fidx.cpu().numpy()[sure], ridx[sure])
+    assert sure.mean() > 0.99

@@ -351,6 +351,36 @@ def test_ops_after_a_large_kernel(gpu, k, layout):
             assert torch.equal(a, b), f"{name}: differs after a large kernel"
 
 
+# every hand-counted store pattern of the window tile kernel (sweep_wave.hip wave_body's ST): one chunk
+# (4 scan passes), one chunk + the remainder diagonal (REM), two chunks (2 passes), four chunks + REM
+# (1 pass), fp32 (dword stores when the block base is unaligned) and fp16 (camera preload)
+TILE_VARIANTS = [(64, torch.float32), (100, torch.float32), (256, torch.float32), (256, torch.float16),
+                 (10, torch.float16)]
+
+
+@pytest.mark.parametrize("D,dtype", TILE_VARIANTS, ids=[f"D{d}_{str(t)[6:]}" for d, t in TILE_VARIANTS])
+@pytest.mark.parametrize("k", [5, 11])
+def test_tile_variants_after_a_large_kernel(gpu, k, D, dtype):
+    """The tile kernel's volume, argmax and soft-argmax variants right after a large kernel equal the same
+    call run warm, bit for bit (each variant's vmcnt waits count its own stores)."""
+    H, W = 18, D + 40
+    cam, proj = make_pair(H, W, D, seed=31, kind="textured")
+    c, p = _dev(cam, gpu).to(dtype), _dev(proj, gpu).to(dtype)
+    ops = {
+        "forward": lambda: [cm.cost_volume_forward(c, p, D, k, WIN, "fast")],
+        "disparity": lambda: list(cm.stereo_disparity(c, p, D, k, WIN)),
+        "soft": lambda: [x for x in cm.stereo_disparity_soft(c, p, D, k, WIN) if torch.is_tensor(x)],
+    }
+    for name, op in ops.items():
+        op()
+        ref = [x.clone() for x in op()]
+        _cold_caches(gpu)
+        got = op()
+        assert len(got) == len(ref) > 0
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b), f"{name}: differs after a large kernel"
+
+
 @pytest.mark.parametrize("case", BWD_CASES, ids=[f"{c[0]}x{c[1]}_k{c[2]}_D{c[3]}_{c[4]}" for c in BWD_CASES])
 @pytest.mark.parametrize("layout", [FULL, WIN])
 def test_backward_given_volume(gpu, case, layout):
@@ -641,109 +671,6 @@ def test_disparity_soft_argmax_and_mask(gpu, case, kind):
     w = np.arange(ref.shape[1], dtype=np.float32)
     want = ((-ridx if layout == "window" else w - ridx) * (rbest > thr)).astype(np.float32)
     assert np.array_equal(dmap.cpu().numpy(), want)
-
-
-# ---- the split forward (capi.hip forward_split): a >= 1 GB window volume is swept as two half-band
-# launches on two streams, the second half's statistics pass beside the first half's sweep ----
-
-def _split_inputs(gpu):
-    H, W, D, k = 1024, 1280, 256, 11  # [1024, 1024, 257] fp32 = 1.08 GB
-    cam, proj = make_pair(H, W, D, seed=61)
-    return _dev(cam, gpu, torch.float16), _dev(proj, gpu, torch.float16), H, D, k
-
-
-def test_split_forward_matches_half_bands(gpu, monkeypatch):
-    """The two-stream forward equals the same rows computed as two separate band calls (each below the
-    split size), bit for bit, and stays within the fast tolerance of the exact volume."""
-    monkeypatch.setenv("CUSTMA_FWD_SPLIT", "1")  # opt-in (slower than the single stream, DESIGN §3.1)
-    c, p, H, D, k = _split_inputs(gpu)
-    full = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
-    torch.cuda.synchronize()
-    r0, r1 = k // 2, k - 1 - k // 2
-    for b, e in ((0, 300), (300, 700), (700, H)):
-        a0, a1 = max(0, b - r0), min(H, e + r1)
-        vb = cm.cost_volume_forward(c[a0:a1].contiguous(), p[a0:a1].contiguous(), D, k, WIN, "fast",
-                                    rows=(b - a0, e - a0))
-        assert torch.equal(vb, full[b:e]), (b, e)
-        del vb
-    for h0 in (0, 509, 1016):
-        ex = cm.cost_volume_forward(c[max(0, h0 - r0):h0 + 8 + r1].contiguous(),
-                                    p[max(0, h0 - r0):h0 + 8 + r1].contiguous(), D, k, WIN, "exact",
-                                    rows=(h0 - max(0, h0 - r0), h0 - max(0, h0 - r0) + 8))
-        assert float((ex - full[h0:h0 + 8]).abs().max()) <= O.fast_tolerance(k)
-
-
-def test_split_forward_graph_capture(gpu, monkeypatch):
-    """Under stream capture the forward records its single-stream form (capi.hip: the side-stream
-    split is for eager calls): a replay on new inputs equals the eager (split) forward bit for bit."""
-    monkeypatch.setenv("CUSTMA_FWD_SPLIT", "1")
-    c, p, H, D, k = _split_inputs(gpu)
-    out = torch.empty(H, c.shape[1] - D, D + 1, device=gpu)
-    side = torch.cuda.Stream(gpu)
-    side.wait_stream(torch.cuda.current_stream(gpu))
-    with torch.cuda.stream(side):
-        cm.cost_volume_forward(c, p, D, k, WIN, "fast", out=out)  # warm-up outside the capture
-    torch.cuda.current_stream(gpu).wait_stream(side)
-    torch.cuda.synchronize(gpu)
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        cm.cost_volume_forward(c, p, D, k, WIN, "fast", out=out)
-    c2, p2 = make_pair(H, c.shape[1], D, seed=62)
-    with torch.no_grad():
-        c.copy_(_dev(c2, gpu, torch.float16))
-        p.copy_(_dev(p2, gpu, torch.float16))
-    graph.replay()
-    torch.cuda.synchronize(gpu)
-    ref = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
-    assert torch.equal(out, ref)
-
-
-# ---- the fused forward (sweep_wave.hip k_fwd_tile FUSED): the statistics tiles run in the sweep's own
-# launch, each band's sweep tiles waiting on a per-band counter (large window volumes, 64-row bands) ----
-
-FUSED_CASES = [
-    (1280, 2048, 256, 11, torch.float16),  # C3-like: D = 256, four chunks + the remainder diagonal
-    (1216, 2048, 200, 4, torch.float16),   # no remainder diagonal; even k
-    (1280, 2048, 250, 16, torch.float32),  # fp32 images, the largest even sliding k
-    (1344, 2080, 256, 3, torch.float16),   # 2080 % 32 == 0, k = 3 (the smallest fused k)
-]
-
-
-@pytest.mark.parametrize("form", ["1", "2"], ids=["sc1", "acquire"])
-@pytest.mark.parametrize("case", FUSED_CASES, ids=[f"{c[0]}x{c[1]}_D{c[2]}_k{c[3]}" for c in FUSED_CASES])
-def test_fused_forward_matches_separate_statistics(gpu, monkeypatch, case, form):
-    """The fused launch (CUSTMA_FWD_FUSED=1) writes the volume bit for bit as the separate statistics
-    pass + sweep do, also when replayed from a hipGraph; sampled rows stay within the fast tolerance
-    of the exact volume."""
-    H, W, D, k, dt = case
-    cam, proj = make_pair(H, W, D, seed=71)
-    c, p = _dev(cam, gpu, dt), _dev(proj, gpu, dt)
-    sep = cm.cost_volume_forward(c, p, D, k, WIN, "fast")  # default: separate statistics pass, one sweep
-    monkeypatch.setenv("CUSTMA_FWD_FUSED", form)  # opt-in (measured slower, DESIGN §3.1)
-    fused = cm.cost_volume_forward(c, p, D, k, WIN, "fast")
-    torch.cuda.synchronize()
-    assert torch.equal(fused, sep)
-    del sep
-    out = torch.empty_like(fused)
-    s = torch.cuda.Stream(gpu)
-    s.wait_stream(torch.cuda.current_stream(gpu))
-    with torch.cuda.stream(s):
-        cm.cost_volume_forward(c, p, D, k, WIN, "fast", out=out)
-    torch.cuda.current_stream(gpu).wait_stream(s)
-    graph = torch.cuda.CUDAGraph()
-    out.zero_()
-    with torch.cuda.graph(graph):
-        cm.cost_volume_forward(c, p, D, k, WIN, "fast", out=out)
-    graph.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(out, fused)
-    del out, graph
-    r0, r1 = k // 2, k - 1 - k // 2
-    for h0 in (0, 64 * 7 - 3, H - 8):
-        a0 = max(0, h0 - r0)
-        ex = cm.cost_volume_forward(c[a0:h0 + 8 + r1].contiguous(), p[a0:h0 + 8 + r1].contiguous(), D, k, WIN,
-                                    "exact", rows=(h0 - a0, h0 - a0 + 8))
-        assert float((ex - fused[h0:h0 + 8]).abs().max()) <= O.fast_tolerance(k), h0
 
 
 # ---- workspace contents: no op may read a workspace byte it did not write.  The round-4 and round-5 window

@@ -153,3 +153,45 @@ def test_band_bounds_partition():
             assert spans[0][0] == 0 and spans[-1][1] == H
             assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
             assert max(e - b for b, e in spans) - min(e - b for b, e in spans) <= 1
+
+
+def _reinit_worker(rank, port, port2, H, W, k, D, q):
+    """world 2 with H given (the RowBandGroup is cached), then destroy and re-init world 2 with the
+    ranks swapped: same band height, H and k, so only the group's rank tells the cache entries apart
+    -- a RowBandGroup of the old group would exchange halos with the wrong neighbours (ADVICE r5,
+    rowband._GROUPS)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    from custereomatching_amd.rowband import band_bounds, stereo_matching_rowband
+
+    cam, proj = make_pair(H, W, D, seed=17)
+    be = OracleBackend()
+    out = []
+    for pt, r in ((port, rank), (port2, 1 - rank)):
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{pt}", rank=r, world_size=2)
+        try:
+            b, e = band_bounds(H, 2, r)
+            v = stereo_matching_rowband(torch.from_numpy(cam[b:e].copy()), torch.from_numpy(proj[b:e].copy()), D, k,
+                                        "full", backend=be, H=H)
+            out.append((b, e, v.detach().numpy()))
+        finally:
+            dist.destroy_process_group()
+    q.put((rank, out))
+
+
+def test_rowband_group_cache_after_reinit():
+    H, W, D, k = 12, 16, 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port, port2 = _free_port(), _free_port()
+    procs = [ctx.Process(target=_reinit_worker, args=(r, port, port2, H, W, k, D, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cam, proj = make_pair(H, W, D, seed=17)
+    vol = O.forward(cam, proj, k, layout=O.FULL, D=0)
+    for rank, out in res:
+        for b, e, v in out:
+            assert np.array_equal(v, vol[b:e])
