@@ -58,9 +58,9 @@ extern "C" {
 #define CUSTMA_E_UNSUPPORTED (-5)
 
 /* kernel_size range.  Even k has its taps at offsets -k/2 .. k-1-k/2, exactly as the reference's
- * `kernel_size / 2` origin (stereo_matching_kernel.cu:44,60).  Every k <= 17 and odd k <= 31 run the
- * sliding-window kernels (fused backward, fused disparity; the fast volume up to k = 17, the exact one
- * above -- capi.hip kFastVolumeMaxK); the exact forward has compile-time instantiations up to k = 33;
+ * `kernel_size / 2` origin (stereo_matching_kernel.cu:44,60).  Every k <= 31 runs the sliding-window
+ * kernels (fused backward, fused disparity; the fast volume up to k = 11, where it stays within 1e-5 of
+ * the reference, the exact one above -- capi.hip kFastVolumeMaxK); the exact forward has compile-time instantiations up to k = 33;
  * other sizes up to CUSTMA_MAX_KERNEL run the runtime-k exact forward and the generic fp64 backward. */
 #define CUSTMA_MAX_KERNEL 63
 
@@ -88,7 +88,7 @@ int custma_forward(const void* camera, const void* projector, int32_t dtype, int
  * (custma/src/stereo_matching_kernel.cu:75-179, :218-261).  Deterministic (no atomics).
  * `cost_volume` is the forward's output for the same images (the autograd op keeps it); NULL makes
  * the call recompute it into the workspace exactly as custma_forward(precision FAST) returns it (the
- * sliding fp64 volume up to k = 17, the exact one above; size the workspace with
+ * sliding fp64 volume up to k = 11, the exact one above; size the workspace with
  * CUSTMA_OP_BACKWARD_RECOMPUTE).
  * Window layouts with D = 64 n recompute the last diagonal's cost from the images rather than read
  * it (one 128-byte line per voxel saved), as the reference recomputes every voxel's cost.

@@ -16,6 +16,8 @@ VARIANTS = {
     # knock-out (timing only, wrong results): k_bwd_coop without its volume loads -- the most an in-sweep
     # recompute of the costs could save
     "ko_novol": (["CUSTMA_KO_NOVOL"], BWD),
+    # the full-layout sweep with its round-5 dword volume stores (A/B against the 16-byte stores, round 6)
+    "sweep_dword": (["CUSTMA_SWEEP_NO_X4"], ["sweep_fwd.hip"]),
     # statistics tile: 32 x 32 pixels, 4 rows per thread is the default (profiles/r03/stats)
     "stats32x8": (["CUSTMA_STATS_TX=32", "CUSTMA_STATS_PR=8"], ["stats.hip"]),
     "stats16x8": (["CUSTMA_STATS_TX=16", "CUSTMA_STATS_PR=8"], ["stats.hip"]),

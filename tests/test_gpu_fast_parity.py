@@ -1,12 +1,14 @@
-"""Parity hardening of the default fast volume where its worst-case bound passes 1e-5.
+"""Parity hardening of the default fast volume near its accuracy limit.
 
 The fast sweep's numerator is exact (fp64 sliding sums of exact products); it differs from the reference only
-by the reference's own fp32 rounding, bounded by (k^2 + 6) 2^-24 -- which exceeds north_star's 1e-5 from
-k = 13 on.  `capi.hip` keeps the fast volume up to kFastVolumeMaxK = 17 because the measured difference stays
-far below the bound.  These tests measure it at 256 x 512 (both layouts) on the inputs where fp32 chains
-round worst: quantized-smooth images (verify.py:138-139's preprocessing), large flat regions, and a constant
-plus 1e-4 noise.  The reference arithmetic at full size is the exact forward (bit-identical to the C oracle:
-tests/test_gpu_parity.py::test_exact_forward_bit_identical, re-anchored here on an oracle band).
+by the reference's own fp32 rounding, estimated at (k^2 + 6) 2^-24 -- 7.6e-6 at k = 11, past north_star's 1e-5
+from k = 13 on.  Measured on the inputs where the fp32 chains round worst (profiles/r06/b/diag_fastk.jsonl:
+piecewise-flat 8-bit images, quantized-smooth images as verify.py:138-139's preprocessing makes, a constant
+plus 1e-4 noise) the difference reached 9.5e-6 / 1.26e-5 / 2.08e-5 at k = 13 / 15 / 17, so `capi.hip`
+kFastVolumeMaxK is 11: a `fast` request for a larger k writes the exact volume.  These tests check both
+sides of that limit at 256 x 512 in both layouts against the reference arithmetic at full size -- the exact
+forward, bit-identical to the C oracle (tests/test_gpu_parity.py::test_exact_forward_bit_identical) and
+re-anchored here on an oracle band.
 
 Also the drop-in argmax story (verify.py:72): torch.max over the `exact` volume is the oracle's argmax bit for
 bit; over the default `fast` volume it agrees wherever the top-2 gap exceeds twice the fast bound (the
@@ -55,8 +57,10 @@ def _ill_pair(H, W, D, kind):
 
 @pytest.mark.parametrize("layout,D", [("window", 64), ("full", 0)])
 @pytest.mark.parametrize("kind", ["quantized", "flat", "const_eps"])
-@pytest.mark.parametrize("k", [13, 15, 17])
-def test_fast_volume_within_1e5_at_k13_to_17(gpu, k, kind, layout, D):
+@pytest.mark.parametrize("k", [9, 11, 13, 15, 17])
+def test_fast_volume_within_1e5_near_the_limit(gpu, k, kind, layout, D):
+    """k <= 11: the fast sweep within 1e-5 of the reference arithmetic; k = 13..17 (past the limit): the
+    `fast` request returns the exact volume bit for bit."""
     H, W = 256, 512
     cam, proj = _ill_pair(H, W, max(D, 16), kind)
     c, p = _dev(cam, gpu), _dev(proj, gpu)
@@ -68,6 +72,9 @@ def test_fast_volume_within_1e5_at_k13_to_17(gpu, k, kind, layout, D):
     lay, Dl = (O.FULL, 0) if layout == "full" else (O.WINDOW, D)
     ref = O.forward(cam[h0 - o:h1 + a], proj[h0 - o:h1 + a], k, layout=lay, D=Dl)[o:o + h1 - h0]
     assert np.array_equal(ex[h0:h1].cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    if k > 11:
+        assert torch.equal(fa, ex)
+        return
     err = float((fa - ex).abs().max())
     assert err <= 1e-5, f"fast volume {err:.3g} from the reference arithmetic (k = {k}, {kind}, {layout})"
 

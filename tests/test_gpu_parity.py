@@ -47,7 +47,7 @@ CASES = [
     (30, 64, 15, 31, "quantized"),
     (24, 48, 7, 0, "textured"),
     (26, 40, 5, 39, "textured"),
-    # odd k > 17: the volume is the exact kernel's (the fast volume stops at k = 17, capi.hip
+    # k > 11: the volume is the exact kernel's (the fast volume stops at k = 11, capi.hip
     # kFastVolumeMaxK); the sliding instantiations up to k = 31 serve the disparity and backward
     (19, 37, 21, 9, "textured"),
     (22, 60, 31, 12, "textured"),
@@ -386,7 +386,7 @@ def test_tile_variants_after_a_large_kernel(gpu, k, D, dtype):
 def test_backward_given_volume(gpu, case, layout):
     """The backward handed the forward's volume (the autograd path) against the fp64 oracle, and equal to
     the recompute path (cost_volume=None: the volume rebuilt in the workspace, as the forward builds it --
-    the fast sweep up to k = 17, the exact kernel above) bit for bit."""
+    the fast sweep up to k = 11, the exact kernel above) bit for bit."""
     H, W, k, D, kind = case
     cam, proj = make_pair(H, W, max(D, 1), seed=31, kind=kind)
     lay, Dl = _layout_args(layout, D)
