@@ -122,10 +122,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
 def build_variant(libdir: str, defines, only=None) -> str:
     """Ablation build (benchmarking only): the same library with extra -D switches into
     another directory; load it with CUSTMA_LIB=<path>.  `only`: the translation units the
-    switches affect (the rest link from the main build's objects)."""
+    switches affect, by source file or unit name (the rest link from the main build's objects)."""
     os.makedirs(libdir, exist_ok=True)
     extra = [d if d.startswith("-") else f"-D{d}" for d in defines]  # "-f..." flags pass through
-    todo = [u for u in UNITS if only is None or u[1] in only]
+    todo = [u for u in UNITS if only is None or u[1] in only or u[0] in only]
     if only is not None:
         build()
     with cf.ThreadPoolExecutor(max_workers=max(1, min(len(todo), os.cpu_count() or 4))) as ex:

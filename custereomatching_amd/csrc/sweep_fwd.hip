@@ -43,6 +43,10 @@ namespace {
 
 typedef __attribute__((address_space(3))) volatile double lds_vd;
 constexpr int kFwdNST = 2;  // loader register stages (x loads per step <= 63 + one step)
+#ifndef CUSTMA_SWEEP_AUX
+#define CUSTMA_SWEEP_AUX kStoreAux
+#endif
+constexpr int kSweepAux = CUSTMA_SWEEP_AUX;  // volume store policy (A/B builds set CUSTMA_SWEEP_AUX)
 
 
 template <int K, int TWT, typename T, bool ARGMAX>
@@ -311,7 +315,8 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
 #pragma unroll
         for (int m = 0; m < TWT; ++m) v[m] = *(const float*)(tile + voff[m] + 4 * (m * stgA + stgB));
 #pragma unroll
-        for (int m = 0; m < TWT; ++m) st_vol(v[m], rOut, voff[m]);
+        for (int m = 0; m < TWT; ++m)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v[m]), rOut, voff[m], 0, kSweepAux);
     };
 
     __syncthreads();  // the loader's first stage

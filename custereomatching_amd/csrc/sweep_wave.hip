@@ -718,7 +718,10 @@ WaveGrid wave_grid(const Geo& g) {
     wg.rem = g.layout == CUSTMA_LAYOUT_WINDOW && nd > 64 && nd % 64 == 1;
     if (wg.rem) --wg.nChunk;
     wg.nTile = (int)cdiv(g.WO, TW);
-    wg.TH = 64;  // band height (32 / 128 measured within 2 %)
+#ifndef CUSTMA_WAVE_TH
+#define CUSTMA_WAVE_TH 64
+#endif
+    wg.TH = CUSTMA_WAVE_TH;  // band height (32 / 128 measured within 2 %; A/B builds set CUSTMA_WAVE_TH)
     // keep >= ~8 waves per SIMD on small problems
     while (wg.TH > 8 && (int64_t)wg.nTile * wg.nChunk * cdiv(g.HV(), wg.TH) < 8192) wg.TH /= 2;
     wg.nBand = (int)cdiv(g.HV(), wg.TH);
