@@ -392,7 +392,7 @@ def main():
     # library on the op's stream; custma_profile_*), for the roofline figures
     _lib.profile_enable(True)
     if distributed:
-        rowband.enable_timing(args.dist_backend == "nccl")
+        rowband.enable_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timed=True)
@@ -415,7 +415,10 @@ def main():
         mine = {"rank": rank, "rows": int(cam.shape[0]), "fwd_sweep_launch_ms": round(fwd_kms, 4),
                 "fwd_sweep_launches_per_step": round(n_fk / max(1, args.steps), 2),
                 "bwd_sweep_launch_ms": round(bwd_kms, 4), "step_ms_local": round(elapsed / args.steps * 1e3, 4)}
-        mine.update(rowband.timing_summary() if args.dist_backend == "nccl" else {})
+        # (gloo rehearsal: the halos are staged through host memory, so these spans include the device-host
+        # copies and the host wait -- a rehearsal of the bookkeeping, not an xGMI figure)
+        mine.update(rowband.timing_summary())
+        mine["exchange_transport"] = "rccl (device to device)" if args.dist_backend == "nccl" else "gloo (host-staged)"
         rowband.enable_timing(False)
         per_rank = [None] * world
         dist.all_gather_object(per_rank, mine)

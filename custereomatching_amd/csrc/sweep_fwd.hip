@@ -367,71 +367,88 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 // layout index s of diagonal lane l for camera column u0 + m
                 const float sbase = (float)(window ? d0 : u0 + m + d0);
                 const float* rowp = stg + (red_live ? m : 0) * NLP;
-                // Two passes over the row's diagonals l = part_i + TPR e (nsc per lane, no bound test: columns
-                // NL .. NLP - 1 hold -FLT_MAX, which changes none of the results, so the reads batch up).
-                // Pass 1: the top two VALUES (exact floats, duplicates count) by v_max / v_med3, 2 VALU per
-                // element; the TPR lanes merged by DPP (quad xor 1, xor 2, half-row mirror, row mirror: each
-                // lane meets every other lane's part once).  Pass 2, the column's best known: the first
-                // diagonal holding it (v == best: the first index wins among equal values) and the
-                // soft-argmax sums weighted relative to it (no rescaling).  Round 5 did both in one pass
-                // (a compare, three selects and a rescaled exp2 per element; a four-way compare per merge).
+                // nsc diagonals per lane, no bound test: the row's columns NL .. NLP - 1 hold -FLT_MAX
+                // (written once, below the loader split), which changes none of the results, so the LDS
+                // reads batch up instead of one exec-masked, waited read per element.
                 const int nsc = (NL + TPR - 1) / TPR;
-                float best = -FLT_MAX, second = -FLT_MAX;
-#pragma unroll 4
-                for (int e = 0; e < nsc; ++e) {
-                    const float v = red_live ? rowp[part_i + TPR * e] : -FLT_MAX;
-                    second = __builtin_amdgcn_fmed3f(best, second, v);  // best >= second: the new second
-                    best = __builtin_fmaxf(best, v);
-                }
                 auto mvf = [&](float x, auto ctl) {
                     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x),
                                                                                  decltype(ctl)::value, 0xf, 0xf, false));
-                };
-                auto merge2 = [&](auto ctl) {
-                    const float ob = mvf(best, ctl), os = mvf(second, ctl);
-                    second = __builtin_amdgcn_fmed3f(best, ob, __builtin_fmaxf(second, os));  // top two of four
-                    best = __builtin_fmaxf(best, ob);
                 };
                 typedef std::integral_constant<int, 0xB1> X1;   // quad_perm [1,0,3,2]
                 typedef std::integral_constant<int, 0x4E> X2;   // quad_perm [2,3,0,1]
                 typedef std::integral_constant<int, 0x141> HM;  // row_half_mirror
                 typedef std::integral_constant<int, 0x140> RM;  // row_mirror
-                if (TPR >= 2) merge2(X1{});
-                if (TPR >= 4) merge2(X2{});
-                if (TPR >= 8) merge2(HM{});
-                if (TPR >= 16) merge2(RM{});
-                int fe = 0x7fffffff;   // the first e with row[part_i + TPR e] == best (this lane)
-                float q0 = 0.f, qe = 0.f;  // soft: sum w, sum e w (w = exp2(kb (v - best)))
-                const float nkb = best > -FLT_MAX ? -part.kb * best : 0.f;  // (no value: every w = 0)
-                auto pass2 = [&](auto soft_c) {
-                    constexpr bool SOFTC = decltype(soft_c)::value;
+                // the TPR lanes of a column combined by DPP (quad xor 1, xor 2, half-row mirror, row mirror:
+                // each lane meets every other lane's part once)
+                auto over_tpr = [&](auto f) {
+                    if (TPR >= 2) f(X1{});
+                    if (TPR >= 4) f(X2{});
+                    if (TPR >= 8) f(HM{});
+                    if (TPR >= 16) f(RM{});
+                };
+                float best = -FLT_MAX, second = -FLT_MAX, q0 = 0.f, q1 = 0.f;
+                int bi = 0x7fffffff;
+                if (soft) {
+                    // Two passes (round 6, as the tile kernel's soft scan, sweep_wave.hip): the top two values
+                    // by v_max / v_med3, then the first diagonal holding the best and the soft sums weighted
+                    // relative to it (no running rescale).  C2 full soft 2.58 -> 2.27 ms; the plain argmax
+                    // keeps the one-pass scan (two passes: 1.84 -> 2.07 ms, profiles/r06/c).
+#pragma unroll 4
+                    for (int e = 0; e < nsc; ++e) {
+                        const float v = red_live ? rowp[part_i + TPR * e] : -FLT_MAX;
+                        second = __builtin_amdgcn_fmed3f(best, second, v);  // best >= second: the new second
+                        best = __builtin_fmaxf(best, v);
+                    }
+                    over_tpr([&](auto ctl) {
+                        const float ob = mvf(best, ctl), os = mvf(second, ctl);
+                        second = __builtin_amdgcn_fmed3f(best, ob, __builtin_fmaxf(second, os));  // top two of four
+                        best = __builtin_fmaxf(best, ob);
+                    });
+                    int fe = 0x7fffffff;  // the first e with row[part_i + TPR e] == best (this lane)
+                    float qe = 0.f;       // sum of e w (w = exp2(kb (v - best)); q0 = sum of w)
+                    const float nkb = best > -FLT_MAX ? -part.kb * best : 0.f;  // (no value: every w = 0)
 #pragma unroll 4
                     for (int e = nsc - 1; e >= 0; --e) {
                         const float v = red_live ? rowp[part_i + TPR * e] : -FLT_MAX;
                         fe = v == best ? e : fe;
-                        if constexpr (SOFTC) {
-                            const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(part.kb, v, nkb));
-                            q0 += w;
-                            qe = __builtin_fmaf(w, (float)e, qe);
-                        }
+                        const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(part.kb, v, nkb));
+                        q0 += w;
+                        qe = __builtin_fmaf(w, (float)e, qe);
                     }
-                };
-                if (soft) pass2(std::true_type{});
-                else pass2(std::false_type{});
-                int bi = fe == 0x7fffffff || !(best > -FLT_MAX) ? 0x7fffffff : part_i + TPR * fe;
-                // sum over the lane's diagonals of s w, s = sbase + part_i + TPR e
-                float q1 = soft ? __builtin_fmaf(sbase + (float)part_i, q0, (float)TPR * qe) : 0.f;
-                auto merge1 = [&](auto ctl) {
-                    bi = min(bi, __builtin_amdgcn_update_dpp(0, bi, decltype(ctl)::value, 0xf, 0xf, false));
-                    if (soft) {
+                    bi = fe == 0x7fffffff || !(best > -FLT_MAX) ? 0x7fffffff : part_i + TPR * fe;
+                    // sum over the lane's diagonals of s w, s = sbase + part_i + TPR e
+                    q1 = __builtin_fmaf(sbase + (float)part_i, q0, (float)TPR * qe);
+                    over_tpr([&](auto ctl) {
+                        bi = min(bi, __builtin_amdgcn_update_dpp(0, bi, decltype(ctl)::value, 0xf, 0xf, false));
                         q0 += mvf(q0, ctl);
                         q1 += mvf(q1, ctl);
+                    });
+                } else {
+                    // one pass: each lane scans its diagonals in increasing order (branch-free: the first
+                    // index wins among equal values); second never holds a NaN (it takes best, or v when
+                    // v > second), so max(second, v) needs no fmaxf NaN handling
+#pragma unroll 4
+                    for (int e = 0; e < nsc; ++e) {
+                        const int l = part_i + TPR * e;
+                        const float v = red_live ? rowp[l] : -FLT_MAX;
+                        const bool gt = v > best;
+                        second = gt ? best : (v > second ? v : second);
+                        bi = gt ? l : bi;
+                        best = gt ? v : best;
                     }
-                };
-                if (TPR >= 2) merge1(X1{});
-                if (TPR >= 4) merge1(X2{});
-                if (TPR >= 8) merge1(HM{});
-                if (TPR >= 16) merge1(RM{});
+                    over_tpr([&](auto ctl) {
+                        const float ob = mvf(best, ctl), os = mvf(second, ctl);
+                        const int oi = __builtin_amdgcn_update_dpp(0, bi, decltype(ctl)::value, 0xf, 0xf, false);
+                        if (ob > best || (ob == best && oi < bi)) {
+                            second = fmaxf(os, best);
+                            best = ob;
+                            bi = oi;
+                        } else {
+                            second = fmaxf(second, ob);
+                        }
+                    });
+                }
                 const int64_t u = u0 + m;
                 if (red_live && part_i == 0 && u < g.WO) {
                     const int64_t pidx = ((int64_t)chunk * g.HV() + (h - g.h_lo)) * g.WO + u;

@@ -412,62 +412,80 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                     for (int ps = 0; ps < AMX; ++ps) {
                         const int m = (ps * nw + wv) * 4 + (l >> 4);  // tile row of this 16-lane group
                         const int mr = m < TW ? m : 0;
-                        // Two passes over the row's D + 1 values (lane sub: columns sub + 16 i), no bound test:
-                        // columns DO .. 16 nsc - 1 hold -FLT_MAX, which changes none of the results, so the reads
-                        // batch up.  Pass 1: the top two VALUES (exact floats; duplicates count, so a tie leaves
-                        // second == best) by v_max / v_med3, 2 VALU per element, the 16 lanes combined by DPP row
-                        // rotations (8, 4, 2, 1: every lane meets each other lane's part once).  Pass 2, with the
-                        // row's best known: the first index holding it (v == best; the first index wins among
-                        // equal values, torch.argmax semantics) and the soft-argmax sums weighted relative to it
-                        // (no rescaling).  Round 5 did both in one pass (compare, three selects and a rescaled
-                        // exp2 per element; a four-way compare per merge level).
+                        // No bound test in the scans: the row's columns DO .. 16 nsc - 1 hold -FLT_MAX, which
+                        // changes none of the results, so the reads batch up (an exec-masked read per element
+                        // waited for each one: the scan was 28 % of the kernel, profiles/r05/k).  Partly
+                        // unrolled: fully unrolled, the compiler hoists all 17 LDS reads (and the soft sums'
+                        // exp2 operands) and the kernel needs 168-206 VGPRs.
                         const int nsc = ((int)DO + 15) >> 4;
                         const lds_vf* row = sb + mr * kAmxPitch + sub;
-                        float b = -FLT_MAX, sec = -FLT_MAX;
+                        auto rot = [&](float x, auto ctl) {
+                            return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                0, __builtin_bit_cast(int, x), decltype(ctl)::value, 0xf, 0xf, false));
+                        };
+                        float b = -FLT_MAX, sec = -FLT_MAX, q0 = 0.f, q1 = 0.f;
+                        int bi = INT_MAX;
+                        if constexpr (SOFT) {
+                            // Two passes (round 6).  Pass 1: the top two VALUES (exact floats; duplicates count,
+                            // so a tie leaves sec == b) by v_max / v_med3, 2 VALU per element, the 16 lanes of the
+                            // row combined by DPP row rotations (8, 4, 2, 1: every lane meets each other lane's
+                            // part once).  Pass 2, the row's best known: the first index holding it (v == b: the
+                            // first index wins among equal values, torch.argmax semantics) and the soft sums
+                            // weighted relative to it, so no running rescale.  C3 soft 1.75 -> 1.40 ms, C5
+                            // 14.4 -> 11.4 ms; the plain argmax measured slower this way (C3 1.24 -> 1.26 ms:
+                            // pass 2 re-reads the row) and keeps the one-pass scan below (profiles/r06/c).
 #pragma unroll 6
-                        for (int i = 0; i < nsc; ++i) {
-                            const float v = row[16 * i];
-                            sec = __builtin_amdgcn_fmed3f(b, sec, v);  // b >= sec: the new second
-                            b = __builtin_fmaxf(b, v);
-                        }
-                        Unroll<0, 4>::run([&](auto lc) {
-                            constexpr int ctrl = 0x120 + (8 >> decltype(lc)::value);  // row_ror:8, 4, 2, 1
-                            auto rot = [&](float x) {
-                                return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                                    0, __builtin_bit_cast(int, x), ctrl, 0xf, 0xf, false));
-                            };
-                            const float ob = rot(b), os = rot(sec);
-                            // the top two of {b, sec, ob, os} (b >= sec, ob >= os)
-                            sec = __builtin_amdgcn_fmed3f(b, ob, __builtin_fmaxf(sec, os));
-                            b = __builtin_fmaxf(b, ob);
-                        });
-                        int fi = INT_MAX;  // the first i with row[16 i] == b (this lane)
-                        float q0 = 0.f, qi = 0.f;  // soft: sum w, sum i w (w = exp2(kb (v - b)))
-                        const float nkb = b > -FLT_MAX ? -kb * b : 0.f;  // (a row without values: every w = 0)
-#pragma unroll SOFT ? 3 : 6
-                        for (int i = nsc - 1; i >= 0; --i) {
-                            const float v = row[16 * i];
-                            fi = v == b ? i : fi;
-                            if constexpr (soft) {
+                            for (int i = 0; i < nsc; ++i) {
+                                const float v = row[16 * i];
+                                sec = __builtin_amdgcn_fmed3f(b, sec, v);  // b >= sec: the new second
+                                b = __builtin_fmaxf(b, v);
+                            }
+                            Unroll<0, 4>::run([&](auto lc) {
+                                const std::integral_constant<int, 0x120 + (8 >> decltype(lc)::value)> ctl;  // row_ror
+                                const float ob = rot(b, ctl), os = rot(sec, ctl);
+                                sec = __builtin_amdgcn_fmed3f(b, ob, __builtin_fmaxf(sec, os));  // top two of four
+                                b = __builtin_fmaxf(b, ob);
+                            });
+                            int fi = INT_MAX;  // the first i with row[16 i] == b (this lane)
+                            float qi = 0.f;    // sum of i w (w = exp2(kb (v - b)); q0 = sum of w)
+                            const float nkb = b > -FLT_MAX ? -kb * b : 0.f;  // (a row without values: every w = 0)
+#pragma unroll 3
+                            for (int i = nsc - 1; i >= 0; --i) {
+                                const float v = row[16 * i];
+                                fi = v == b ? i : fi;
                                 const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(kb, v, nkb));
                                 q0 += w;
                                 qi = __builtin_fmaf(w, (float)i, qi);
                             }
-                        }
-                        int bi = fi == INT_MAX || !(b > -FLT_MAX) ? INT_MAX : sub + 16 * fi;
-                        float q1 = soft ? __builtin_fmaf((float)sub, q0, 16.f * qi) : 0.f;  // sum s w, s = sub + 16 i
-                        Unroll<0, 4>::run([&](auto lc) {
-                            constexpr int ctrl = 0x120 + (8 >> decltype(lc)::value);
-                            bi = min(bi, __builtin_amdgcn_update_dpp(0, bi, ctrl, 0xf, 0xf, false));
-                            if constexpr (soft) {
-                                auto rot = [&](float x) {
-                                    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                                        0, __builtin_bit_cast(int, x), ctrl, 0xf, 0xf, false));
-                                };
-                                q0 += rot(q0);
-                                q1 += rot(q1);
+                            bi = fi == INT_MAX || !(b > -FLT_MAX) ? INT_MAX : sub + 16 * fi;
+                            q1 = __builtin_fmaf((float)sub, q0, 16.f * qi);  // sum of s w, s = sub + 16 i
+                            Unroll<0, 4>::run([&](auto lc) {
+                                const std::integral_constant<int, 0x120 + (8 >> decltype(lc)::value)> ctl;
+                                bi = min(bi, __builtin_amdgcn_update_dpp(0, bi, decltype(ctl)::value, 0xf, 0xf, false));
+                                q0 += rot(q0, ctl);
+                                q1 += rot(q1, ctl);
+                            });
+                        } else {
+                            // one scan chain per lane (increasing s: the first index wins among equal values),
+                            // then the 16 lanes of the row combined by DPP row rotations (8, 4, 2, 1).  sec never
+                            // holds a NaN (it takes b, or v when v > sec), so max(sec, v) needs no NaN handling.
+#pragma unroll 6
+                            for (int i = 0; i < nsc; ++i) {
+                                const int s2 = sub + 16 * i;
+                                const float v = row[16 * i];
+                                const bool gt = v > b;
+                                sec = gt ? b : (v > sec ? v : sec);
+                                bi = gt ? s2 : bi;
+                                b = gt ? v : b;
                             }
-                        });
+                            Unroll<0, 4>::run([&](auto lc) {
+                                const std::integral_constant<int, 0x120 + (8 >> decltype(lc)::value)> ctl;
+                                const float ob = rot(b, ctl), os = rot(sec, ctl);
+                                const int oi = __builtin_amdgcn_update_dpp(0, bi, decltype(ctl)::value, 0xf, 0xf, false);
+                                if (ob > b || (ob == b && oi < bi)) { sec = fmaxf(os, b); b = ob; bi = oi; }
+                                else sec = fmaxf(sec, ob);
+                            });
+                        }
                         const uint32_t vo = (sub == 0 && m < TW) ? (uint32_t)(m * 4) : OOB;
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, b), rB, vo, 0u, 0);
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, sec), rS, vo, 0u, 0);
