@@ -49,7 +49,14 @@ constexpr int kFwdNST = 2;  // loader register stages (x loads per step <= 63 + 
 constexpr int kSweepAux = CUSTMA_SWEEP_AUX;  // volume store policy (A/B builds set CUSTMA_SWEEP_AUX)
 
 
-template <int K, int TWT, typename T, bool ARGMAX>
+// X4 (volume form, D_out a multiple of 16, a 16-byte aligned volume): every chunk's owned columns of a row are
+// whole 64-byte sectors (sweep.h owned chunks, beta = 0), so the step's 16 x S owned floats leave as 16-byte
+// stores, a lane taking up to 4 groups of 4 consecutive columns instead of 16 dword stores.  The staging rows
+// are padded (pitch NL + 4) and row m shifted by (m + 1) & 3 floats (full layout), which puts every group on
+// a 16-byte LDS boundary: one conflict-free ds_read_b128 per group.  (Round 6's first form read each group as
+// four ds_read_b32 at a 16-byte lane stride -- bank conflicts -- and measured slower than the dword stores,
+// profiles/r06/b; the bare store patterns: 0.954 ms dword vs 0.850 ms x4 at C2 full, profiles/r06/d.)
+template <int K, int TWT, typename T, bool ARGMAX, bool X4 = false>
 __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                    Stats sc, Stats sp, float* __restrict__ out, SweepGrid sg,
                                                    DispPartial part) {
@@ -59,6 +66,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     static_assert(TWT == 16 && NX <= 48, "row-broadcast layout assumes 16 own columns and <= 48 camera columns");
     constexpr int NL_MAX = 320, LO = (NX + NL_MAX - 1 + 63) / 64, LS = (TWT + NL_MAX - 1 + 63) / 64;
     const int NL = sg.NL, NO = NX + NL - 1, NS = TWT + NL - 1;
+    const int NLS = X4 ? NL + 4 : NL;  // staging row pitch of the volume form
     // LDS rows are padded to whole loader-lane chunks (OP = 64 LO, SP = 64 LS), so the loader
     // writes every lane of every chunk unconditionally (the padding takes zeros / ignored
     // values): its step is straight-line code, which keeps three steps of loads in flight
@@ -70,7 +78,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     double* usB = rsM + 2 * SP;            // [2][64]  -(camera fp64 patch sums) (lanes 0-15)
     float* rsQ = (float*)(usB + 2 * 64);   // [2][SP]  projector ey2
     float* usQ = rsQ + 2 * SP;             // [2][64]  camera ex2 (lanes 0-15)
-    float* stg = usQ + 2 * 64;             // [2][16][NL] cost tile staging (ARGMAX: [16][NL] reduction)
+    float* stg = usQ + 2 * 64;             // [2][16][NLS] cost tile staging (ARGMAX: [16][NL] reduction)
 
     const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);
     const int chunk = (int)(bid % sg.nChunk);
@@ -293,8 +301,8 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     // Per lane and tile row m: byte offset of its volume element inside the row tile
     // (out of range for lanes past the owned columns); the staging slot of that element
     // is the same offset plus a per-row constant.
-    uint32_t voff[TWT];
-    {
+    uint32_t voff[X4 ? 1 : TWT];
+    if constexpr (!X4) {
         const bool phase_fixed = ((g.WO * g.DO) & 15) == 0;
         const int r0 = (int)((((h0 - g.h_lo) * g.WO + u0)) & 15), dm = phase_fixed ? DO & 15 : 0;
 #pragma unroll
@@ -308,15 +316,39 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
     // staging index of column c in row m: m*NL + c - d0 - (u0 + m) (full) / m*NL + c - d0
     // (window); with c = voff/4 - m*DO that is voff/4 + m*stgA + stgB
     const int stgA = NL - DO - (window ? 0 : 1), stgB = -(int)d0 - (window ? 0 : (int)u0);
+    // X4: staging row m starts (m + 1) & 3 floats in (full layout; window: 0), so that the 4-column groups,
+    // which start on owned sector boundaries, sit on 16-byte LDS boundaries
+    auto stg_shift = [&](int m) { return window ? 0 : ((m + 1) & 3); };
+    constexpr int NG = X4 ? TWT / 4 : 1;  // groups per lane: ceil(TWT S / (4 NL)) <= TWT / 4 (S <= NL)
+    uint32_t gvo[NG], gso[NG];
+    if constexpr (X4) {
+        const int gpr = sg.S / 4, cb = bound(chunk, 0), ce = bound(chunk + 1, 0);
+#pragma unroll
+        for (int i = 0; i < NG; ++i) {
+            const int q = tid + NL * i, m = q / gpr, c = cb + 4 * (q - m * gpr);
+            const bool ok = m < TWT && u0 + m < g.WO && c < ce;
+            gvo[i] = ok ? (uint32_t)((m * DO + c) * 4) : OOB;
+            gso[i] = ok ? (uint32_t)((m * NLS + stg_shift(m) + c - (int)d0 - (window ? 0 : (int)u0 + m)) * 4) : 0u;
+        }
+    }
     auto store_tile = [&](int64_t h, int b) {
         const auto rOut = make_rsrc(out + ((h - g.h_lo) * g.WO + u0) * g.DO, 0x7FFFFFF0u);
-        const char* tile = (const char*)(stg + b * 16 * NL);
-        float v[TWT];
+        const char* tile = (const char*)(stg + b * 16 * NLS);
+        if constexpr (X4) {
+            i32x4 v[NG];
 #pragma unroll
-        for (int m = 0; m < TWT; ++m) v[m] = *(const float*)(tile + voff[m] + 4 * (m * stgA + stgB));
+            for (int i = 0; i < NG; ++i) v[i] = *(const i32x4*)(tile + gso[i]);
 #pragma unroll
-        for (int m = 0; m < TWT; ++m)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v[m]), rOut, voff[m], 0, kSweepAux);
+            for (int i = 0; i < NG; ++i) __builtin_amdgcn_raw_buffer_store_b128(v[i], rOut, gvo[i], 0u, kSweepAux);
+        } else {
+            float v[TWT];
+#pragma unroll
+            for (int m = 0; m < TWT; ++m) v[m] = *(const float*)(tile + voff[m] + 4 * (m * stgA + stgB));
+#pragma unroll
+            for (int m = 0; m < TWT; ++m)
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v[m]), rOut, voff[m], 0,
+                                                      kSweepAux);
+        }
     };
 
     __syncthreads();  // the loader's first stage
@@ -343,7 +375,7 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
             int TPR = 1;
             while (TPR * 2 * TWT <= NL && TPR < 16) TPR *= 2;
             const int NLP = ARGMAX ? NL + TPR : NL;
-            float* srow = stg + (ARGMAX ? 0 : buf * 16 * NL) + tid;
+            float* srow = stg + (ARGMAX ? 0 : buf * 16 * NLS) + tid;
             Unroll<0, TWT>::run([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
                 if (m > 0) s = (s + col[m + K - 1]) - col[m - 1];
@@ -354,6 +386,8 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                 const float c = (float)e * __builtin_amdgcn_rsqf(den2);
                 if constexpr (ARGMAX) {
                     srow[m * NLP] = (m >= m_lo && m < m_hi) ? c : -FLT_MAX;
+                } else if constexpr (X4) {
+                    srow[m * NLS + stg_shift(m)] = c;
                 } else {
                     srow[m * NL] = c;
                 }
@@ -485,16 +519,27 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
     constexpr int NL_MAX = 320, OP = 64 * ((NX + NL_MAX - 1 + 63) / 64), SP = 64 * ((TW + NL_MAX - 1 + 63) / 64);
     const int NL = sg.NL;
     const size_t lds = sizeof(double) * (4 * OP + 4 * 64 + 2 * SP + 2 * 64) +
-                       sizeof(float) * (2 * SP + 2 * 64 + (part ? TW * (NL + 16) : 2 * TW * NL));
+                       sizeof(float) * (2 * SP + 2 * 64 + (part ? TW * (NL + 16) : 2 * TW * (NL + 4)));
     const int64_t blocks = sweep_blocks(sg);
     if (part) {
         hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, true>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam,
                            proj, g, sc, sp, out, sg, *part);
     } else {
         DispPartial none{};
+        // 16-byte stores: every owned segment starts on a 64-byte sector (D_out % 16 == 0, so beta = 0 in every
+        // row) of a 16-byte aligned volume
+#ifdef CUSTMA_SWEEP_NO_X4
+        const bool x4 = false;  // A/B build (scripts/build_ablations.py sweep_dword)
+#else
+        const bool x4 = g.DO % 16 == 0 && (uintptr_t)out % 16 == 0 && sg.S % 16 == 0;
+#endif
         prof_begin(PROF_FWD, s);
-        hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam, proj,
-                           g, sc, sp, out, sg, none);
+        if (x4)
+            hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false, true>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam,
+                               proj, g, sc, sp, out, sg, none);
+        else
+            hipLaunchKernelGGL((k_sweep_fwd<K, TW, T, false>), dim3((unsigned)blocks), dim3(NL + 64), lds, s, cam,
+                               proj, g, sc, sp, out, sg, none);
         prof_end(PROF_FWD, s);
     }
     return hipGetLastError();
