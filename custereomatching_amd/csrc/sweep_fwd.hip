@@ -467,9 +467,14 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                         const int l = part_i + TPR * e;
                         const float v = red_live ? rowp[l] : -FLT_MAX;
                         const bool gt = v > best;
-                        second = gt ? best : (v > second ? v : second);
                         bi = gt ? l : bi;
+#ifdef CUSTMA_SCAN_MED3
+                        second = __builtin_amdgcn_fmed3f(best, second, v);  // best >= second: the new second
+                        best = __builtin_fmaxf(best, v);
+#else
+                        second = gt ? best : (v > second ? v : second);
                         best = gt ? v : best;
+#endif
                     }
                     over_tpr([&](auto ctl) {
                         const float ob = mvf(best, ctl), os = mvf(second, ctl);

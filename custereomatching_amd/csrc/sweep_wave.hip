@@ -474,9 +474,14 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                                 const int s2 = sub + 16 * i;
                                 const float v = row[16 * i];
                                 const bool gt = v > b;
-                                sec = gt ? b : (v > sec ? v : sec);
                                 bi = gt ? s2 : bi;
+#ifdef CUSTMA_SCAN_MED3
+                                sec = __builtin_amdgcn_fmed3f(b, sec, v);  // b >= sec: the new second
+                                b = __builtin_fmaxf(b, v);
+#else
+                                sec = gt ? b : (v > sec ? v : sec);
                                 b = gt ? v : b;
+#endif
                             }
                             Unroll<0, 4>::run([&](auto lc) {
                                 const std::integral_constant<int, 0x120 + (8 >> decltype(lc)::value)> ctl;
