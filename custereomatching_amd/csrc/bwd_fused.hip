@@ -40,6 +40,7 @@
 // stores of fp32 partial sums per diagonal chunk; k_bwd_gather sums the
 // chunks and k_bwd_combine applies the box filters.
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <type_traits>
 #include <utility>
@@ -89,7 +90,14 @@ __host__ __device__ inline ChunkGeo chunk_geo(const Geo& g, int64_t dlo, int j) 
         const int64_t b = g.W - c.d0;
         c.whi = b < g.W ? b : g.W;
     }
-    const int64_t span = c.whi - c.wlo + (g.k - 1), n = span > kSeg ? (span + kSeg - 1) / kSeg : 1;
+    const int64_t span = c.whi - c.wlo + (g.k - 1);
+    int64_t n = span > kSeg ? (span + kSeg - 1) / kSeg : 1;
+    // run_bwd's tail balancing asks for more (narrower) segments, never narrower than the slot-parity
+    // minimum of k + NLB - 1 columns
+    if (g.seg_min > n) {
+        const int64_t nmax = span / (g.k + NLB - 1);
+        n = nmax > n ? (g.seg_min < nmax ? g.seg_min : nmax) : n;
+    }
     c.seg = span > 0 ? (span + n - 1) / n : 1;
     return c;
 }
@@ -1298,7 +1306,7 @@ BwdPlan plan_bwd_uncached(const Geo& g);
 BwdPlan plan_bwd(const Geo& g) {
     struct Entry {
         int64_t H, W, D, h_lo, h_hi;
-        int k, layout;
+        int k, layout, seg_min;
         BwdPlan p;
     };
     static std::mutex mu;
@@ -1307,13 +1315,13 @@ BwdPlan plan_bwd(const Geo& g) {
         std::lock_guard<std::mutex> lk(mu);
         for (const Entry& e : cache)
             if (e.H == g.H && e.W == g.W && e.D == g.D && e.h_lo == g.h_lo && e.h_hi == g.h_hi && e.k == g.k &&
-                e.layout == g.layout)
+                e.layout == g.layout && e.seg_min == g.seg_min)
                 return e.p;
     }
     const BwdPlan p = plan_bwd_uncached(g);
     std::lock_guard<std::mutex> lk(mu);
     if (cache.size() >= 16) cache.erase(cache.begin());
-    cache.push_back(Entry{g.H, g.W, g.D, g.h_lo, g.h_hi, g.k, g.layout, p});
+    cache.push_back(Entry{g.H, g.W, g.D, g.h_lo, g.h_hi, g.k, g.layout, g.seg_min, p});
     return p;
 }
 
@@ -1395,9 +1403,101 @@ BwdPlan plan_bwd_uncached(const Geo& g) {
 }
 
 
+// Workgroups of k_bwd_coop resident at once on the current device (0 if unknown).
+template <int K, bool WIN>
+int coop_slots() {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bwd_coop<K, WIN>, 64 * NWC, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return per * cus;
+}
+
+// Tail balancing of k_bwd_coop's grid.  Its units (chunk, column segment, row group) take equal time, so a
+// launch of U units on `slots` resident workgroups runs ceil(U / slots) rounds; with few rounds the last,
+// partial one costs up to a whole round (a C5 band of 512 rows -- one rank of 8 -- has 2112 units on 512
+// slots: 4.1 rounds, run as 5).  More, narrower column segments fill the rounds at the price of their k - 1
+// halo steps each: pick the minimum segment count (Geo::seg_min) with the best estimate of
+//     (U / slots) / ceil(U / slots) x (span / (span + nseg (k - 1))),
+// changing the default only for a gain above 1 %.  The partial slots and cover lists (BwdPlan::S) do not
+// depend on the segmentation (a chunk's written ranges are the union of its segments'), so the workspace
+// custma_workspace_bytes sized still fits; run_bwd checks that.
+int tail_seg_min_uncached(const Geo& g, int slots);
+int tail_seg_min(const Geo& g, int slots) {
+    struct Entry {
+        int64_t H, W, D, h_lo, h_hi;
+        int k, layout, slots, seg_min;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (const Entry& e : cache)
+            if (e.H == g.H && e.W == g.W && e.D == g.D && e.h_lo == g.h_lo && e.h_hi == g.h_hi && e.k == g.k &&
+                e.layout == g.layout && e.slots == slots)
+                return e.seg_min;
+    }
+    const int n = tail_seg_min_uncached(g, slots);
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache.size() >= 16) cache.erase(cache.begin());
+    cache.push_back(Entry{g.H, g.W, g.D, g.h_lo, g.h_hi, g.k, g.layout, slots, n});
+    return n;
+}
+int tail_seg_min_uncached(const Geo& g, int slots) {
+    if (slots <= 0) return 0;
+    auto score = [&](int seg_min, int* nseg_out) -> double {
+        Geo gg = g;
+        gg.seg_min = seg_min;
+        const BwdPlan p = plan_bwd(gg);
+        if (!p.ok) return -1.0;
+        int64_t units = 0, steps = 0, cols = 0;
+        for (int j = 0; j < p.nChunk; ++j) {
+            const ChunkGeo c = chunk_geo(gg, p.dlo, j);
+            const int ns = chunk_nseg(c, taps_of(gg));
+            units += (int64_t)ns * p.nRG;
+            cols += c.whi - c.wlo;
+            steps += (c.whi - c.wlo) + (int64_t)(ns + 1) * (g.k - 1);  // a segment sweeps its columns + k - 1 steps
+        }
+        if (units <= 0 || steps <= 0) return -1.0;
+        *nseg_out = p.nsegMax;
+        const double rounds = (double)units / slots;
+        return rounds / std::ceil(rounds) * ((double)cols / (double)steps);
+    };
+    int n0 = 0;
+    const double s0 = score(0, &n0);
+    if (s0 <= 0.0) return 0;
+    double best = s0;
+    int pick = 0;
+    for (int n = n0 + 1; n <= n0 + 24; ++n) {
+        int nn = 0;
+        const double sc = score(n, &nn);
+        if (nn < n) break;  // the slot-parity minimum width caps the count
+        if (sc > best) { best = sc; pick = n; }
+    }
+    return best > s0 * 1.01 ? pick : 0;
+}
+
 template <typename T>
-hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp,
-                   float* dcam, float* dproj, void* ws, hipStream_t s) {
+hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* proj, const Geo& g_in, Stats sc,
+                   Stats sp, float* dcam, float* dproj, void* ws, hipStream_t s) {
+    Geo g = g_in;
+    {
+        int slots = 0;
+        const bool win = win_path_ok(g);
+        switch (g.k) {
+#define CUSTMA_K(KK) \
+    case KK: slots = win ? coop_slots<KK, true>() : coop_slots<KK, false>(); break;
+            CUSTMA_SWEEP_KS(CUSTMA_K)
+#undef CUSTMA_K
+            default: break;
+        }
+#ifndef CUSTMA_NO_TAIL  // (A/B build: scripts/build_ablations.py no_tail)
+        g.seg_min = tail_seg_min(g, slots);
+#endif
+        if (g.seg_min > 0 && plan_bwd(g).S != plan_bwd(g_in).S) g.seg_min = 0;  // (never: S is segmentation-free)
+    }
     const BwdPlan p = plan_bwd(g);
     char* w = (char*)ws;
     float* part = (float*)w;

@@ -24,6 +24,8 @@ struct Geo {
     int32_t D;
     int64_t WO, DO; // volume [h_hi - h_lo, WO, DO]
     int64_t h_lo, h_hi;  // volume rows = image rows [h_lo, h_hi) (row bands: the rest is halo)
+    int32_t seg_min = 0;  // fused backward: at least this many column segments per diagonal chunk (run_bwd's
+                          // tail balancing; 0 = segments of up to kSeg columns)
     __host__ __device__ int64_t HV() const { return h_hi - h_lo; }
 };
 

@@ -459,22 +459,17 @@ __global__ __launch_bounds__(384) void k_sweep_fwd(const T* __restrict__ cam, co
                         q1 += mvf(q1, ctl);
                     });
                 } else {
-                    // one pass: each lane scans its diagonals in increasing order (branch-free: the first
-                    // index wins among equal values); second never holds a NaN (it takes best, or v when
-                    // v > second), so max(second, v) needs no fmaxf NaN handling
+                    // one pass: each lane scans its diagonals in increasing order (branch-free: the strict
+                    // compare keeps the first index among equal values; the top two by v_med3 / v_max:
+                    // C2 full 1.79 -> 1.76 ms, profiles/r06/f)
 #pragma unroll 4
                     for (int e = 0; e < nsc; ++e) {
                         const int l = part_i + TPR * e;
                         const float v = red_live ? rowp[l] : -FLT_MAX;
                         const bool gt = v > best;
                         bi = gt ? l : bi;
-#ifdef CUSTMA_SCAN_MED3
                         second = __builtin_amdgcn_fmed3f(best, second, v);  // best >= second: the new second
                         best = __builtin_fmaxf(best, v);
-#else
-                        second = gt ? best : (v > second ? v : second);
-                        best = gt ? v : best;
-#endif
                     }
                     over_tpr([&](auto ctl) {
                         const float ob = mvf(best, ctl), os = mvf(second, ctl);

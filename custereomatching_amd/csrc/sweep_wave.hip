@@ -466,22 +466,18 @@ __device__ __forceinline__ void wave_body(const T* __restrict__ cam, const T* __
                                 q1 += rot(q1, ctl);
                             });
                         } else {
-                            // one scan chain per lane (increasing s: the first index wins among equal values),
-                            // then the 16 lanes of the row combined by DPP row rotations (8, 4, 2, 1).  sec never
-                            // holds a NaN (it takes b, or v when v > sec), so max(sec, v) needs no NaN handling.
+                            // one scan chain per lane (increasing s: the strict compare keeps the first index among
+                            // equal values; the top two by v_med3 / v_max, C3 1.234 -> 1.208 ms against round 5's
+                            // three selects, profiles/r06/f), then the 16 lanes of the row combined by DPP row
+                            // rotations (8, 4, 2, 1).
 #pragma unroll 6
                             for (int i = 0; i < nsc; ++i) {
                                 const int s2 = sub + 16 * i;
                                 const float v = row[16 * i];
                                 const bool gt = v > b;
                                 bi = gt ? s2 : bi;
-#ifdef CUSTMA_SCAN_MED3
                                 sec = __builtin_amdgcn_fmed3f(b, sec, v);  // b >= sec: the new second
                                 b = __builtin_fmaxf(b, v);
-#else
-                                sec = gt ? b : (v > sec ? v : sec);
-                                b = gt ? v : b;
-#endif
                             }
                             Unroll<0, 4>::run([&](auto lc) {
                                 const std::integral_constant<int, 0x120 + (8 >> decltype(lc)::value)> ctl;
@@ -767,6 +763,30 @@ WaveGrid wave_grid(const Geo& g) {
     wg.TH = CUSTMA_WAVE_TH;  // band height (32 / 128 measured within 2 %; A/B builds set CUSTMA_WAVE_TH)
     // keep >= ~8 waves per SIMD on small problems
     while (wg.TH > 8 && (int64_t)wg.nTile * wg.nChunk * cdiv(g.HV(), wg.TH) < 8192) wg.TH /= 2;
+    // Tail balancing of the tile kernel's grid (window, <= 4 chunks): its workgroups take equal time, so
+    // nTile x nBand of them on `slots` resident ones (3 per CU: the kernel's LDS and VGPR budget) run in
+    // ceil(nTile nBand / slots) rounds of TH + k - 1 steps.  With few rounds the partial last one is a large
+    // share (C3: 4.67 rounds at TH = 64), so take the band height in [TH / 2, TH] with the fewest rounds x steps.
+#ifdef CUSTMA_NO_TAIL
+    if (false) {  // A/B build (scripts/build_ablations.py no_tail)
+#else
+    if (g.layout == CUSTMA_LAYOUT_WINDOW && wg.nChunk <= kTileMaxChunks && wg.TH == CUSTMA_WAVE_TH) {
+#endif
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            cus > 0) {
+            const int64_t slots = 3 * (int64_t)cus;
+            auto cost = [&](int th) { return cdiv((int64_t)wg.nTile * cdiv(g.HV(), th), slots) * (th + g.k - 1); };
+            if ((int64_t)wg.nTile * cdiv(g.HV(), wg.TH) < 16 * slots) {
+                int best = wg.TH;
+                for (int th = wg.TH - 1; th >= wg.TH / 2; --th)
+                    if (cost(th) < cost(best)) best = th;
+                wg.TH = best;
+            }
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     wg.nBand = (int)cdiv(g.HV(), wg.TH);
     return wg;
 }
