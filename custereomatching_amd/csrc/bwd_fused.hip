@@ -1415,13 +1415,16 @@ int coop_slots() {
     return per * cus;
 }
 
-// Tail balancing of k_bwd_coop's grid.  Its units (chunk, column segment, row group) take equal time, so a
-// launch of U units on `slots` resident workgroups runs ceil(U / slots) rounds; with few rounds the last,
-// partial one costs up to a whole round (a C5 band of 512 rows -- one rank of 8 -- has 2112 units on 512
-// slots: 4.1 rounds, run as 5).  More, narrower column segments fill the rounds at the price of their k - 1
-// halo steps each: pick the minimum segment count (Geo::seg_min) with the best estimate of
+// Filling the chip in k_bwd_coop's grid.  A launch of U units (chunk, column segment, row group) on `slots`
+// resident workgroups of which U < slots leaves CUs idle (configs[2]'s window at 1024^2, D = 128: 256 units on
+// 512 slots).  There, more and narrower column segments fill the chip at the price of their k - 1 halo steps
+// each: pick the minimum segment count (Geo::seg_min) with the best estimate of
 //     (U / slots) / ceil(U / slots) x (span / (span + nseg (k - 1))),
-// changing the default only for a gain above 1 %.  The partial slots and cover lists (BwdPlan::S) do not
+// changing the default only for a gain above 1 %: configs[2] window backward 0.62 -> 0.52 ms.  With a round or
+// more of units the same estimate also predicted gains for a partial last round (a C5 rank band at N = 8:
+// 33 row groups, 4.1 rounds), but narrower segments measured 2-3 % slower there and at C2 full (their loads,
+// flushes and 64 extra projector columns per segment), so those grids keep the default (profiles/r06/h, i:
+// C5 rank band 3.46 -> 3.38 ms with the restriction).  The partial slots and cover lists (BwdPlan::S) do not
 // depend on the segmentation (a chunk's written ranges are the union of its segments'), so the workspace
 // custma_workspace_bytes sized still fits; run_bwd checks that.
 int tail_seg_min_uncached(const Geo& g, int slots);
@@ -1468,6 +1471,12 @@ int tail_seg_min_uncached(const Geo& g, int slots) {
     int n0 = 0;
     const double s0 = score(0, &n0);
     if (s0 <= 0.0) return 0;
+    {
+        const BwdPlan p = plan_bwd(g);
+        int64_t units = 0;
+        for (int j = 0; j < p.nChunk; ++j) units += (int64_t)chunk_nseg(chunk_geo(g, p.dlo, j), taps_of(g)) * p.nRG;
+        if (units >= slots) return 0;  // the chip is full: narrower segments only add their overheads
+    }
     double best = s0;
     int pick = 0;
     for (int n = n0 + 1; n <= n0 + 24; ++n) {

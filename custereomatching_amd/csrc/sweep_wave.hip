@@ -763,30 +763,9 @@ WaveGrid wave_grid(const Geo& g) {
     wg.TH = CUSTMA_WAVE_TH;  // band height (32 / 128 measured within 2 %; A/B builds set CUSTMA_WAVE_TH)
     // keep >= ~8 waves per SIMD on small problems
     while (wg.TH > 8 && (int64_t)wg.nTile * wg.nChunk * cdiv(g.HV(), wg.TH) < 8192) wg.TH /= 2;
-    // Tail balancing of the tile kernel's grid (window, <= 4 chunks): its workgroups take equal time, so
-    // nTile x nBand of them on `slots` resident ones (3 per CU: the kernel's LDS and VGPR budget) run in
-    // ceil(nTile nBand / slots) rounds of TH + k - 1 steps.  With few rounds the partial last one is a large
-    // share (C3: 4.67 rounds at TH = 64), so take the band height in [TH / 2, TH] with the fewest rounds x steps.
-#ifdef CUSTMA_NO_TAIL
-    if (false) {  // A/B build (scripts/build_ablations.py no_tail)
-#else
-    if (g.layout == CUSTMA_LAYOUT_WINDOW && wg.nChunk <= kTileMaxChunks && wg.TH == CUSTMA_WAVE_TH) {
-#endif
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            cus > 0) {
-            const int64_t slots = 3 * (int64_t)cus;
-            auto cost = [&](int th) { return cdiv((int64_t)wg.nTile * cdiv(g.HV(), th), slots) * (th + g.k - 1); };
-            if ((int64_t)wg.nTile * cdiv(g.HV(), wg.TH) < 16 * slots) {
-                int best = wg.TH;
-                for (int th = wg.TH - 1; th >= wg.TH / 2; --th)
-                    if (cost(th) < cost(best)) best = th;
-                wg.TH = best;
-            }
-        } else {
-            (void)hipGetLastError();
-        }
-    }
+    // (a tail-balanced band height -- the one with the fewest rounds x (TH + k - 1) steps on 3 workgroups per
+    // CU, TH = 61 at C3 -- measured no faster for the volume and 1.7 % slower for the disparity, round 6:
+    // profiles/r06/g)
     wg.nBand = (int)cdiv(g.HV(), wg.TH);
     return wg;
 }

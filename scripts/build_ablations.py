@@ -19,8 +19,8 @@ VARIANTS = {
     # the full-layout sweep with its round-5 dword volume stores (A/B against the 16-byte stores, round 6)
     # the full-layout sweep's volume stores with the default cache policy instead of nt (round 6)
     "sweep_plain": (["CUSTMA_SWEEP_AUX=0"], ["sweep_fwd.hip"]),
-    # without the tail-balanced grids (band height of the tile forward, column segments of the backward sweep)
-    "no_tail": (["CUSTMA_NO_TAIL"], ["sweep_wave_d", "bwd_fused.hip"]),
+    # without the tail-balanced column segments of the backward sweep
+    "no_tail": (["CUSTMA_NO_TAIL"], ["bwd_fused.hip"]),
     # the full-layout sweep with its dword volume stores (A/B against the 16-byte stores, round 6)
     "sweep_dword": (["CUSTMA_SWEEP_NO_X4"], ["sweep_fwd.hip"]),
     # the window tile forward / disparity with 32-row bands (the store pattern's best band, round 6)

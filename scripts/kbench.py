@@ -13,11 +13,12 @@ CFGS = {
     "c3_full": dict(H=2048, W=2048, k=11, D=256, layout="full", dtype=torch.float16),
     "c3_win_d255": dict(H=2048, W=2048, k=11, D=255, layout="window", dtype=torch.float16),
     "c5_win": dict(H=4096, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
-    # one rank's band of configs[4] at N = 2 / 4 / 8 (strong scaling over row bands; whole images of the band's
-    # height stand in for the haloed bands)
-    "c5_r2": dict(H=2048, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
-    "c5_r4": dict(H=1024, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
-    "c5_r8": dict(H=512, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
+    # one rank's band of configs[4] at N = 2 / 4 / 8 (strong scaling over row bands): whole images of the haloed
+    # band's height (owned rows + 2 r) stand in for the bands -- the backward's row groups then match a middle
+    # rank's (33 / 65 / 129 of 16 rows)
+    "c5_r2": dict(H=2058, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
+    "c5_r4": dict(H=1034, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
+    "c5_r8": dict(H=522, W=8192, k=11, D=256, layout="window", dtype=torch.float16),
     # kernel sizes without a sweep instantiation (exact forward + generic fp64 backward)
     "c3_win_k17": dict(H=2048, W=2048, k=17, D=256, layout="window", dtype=torch.float16),
     "c3_win_k16": dict(H=2048, W=2048, k=16, D=256, layout="window", dtype=torch.float16),

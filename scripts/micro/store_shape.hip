@@ -104,8 +104,11 @@ __global__ void k_x4(float* out, int64_t n4) {
     }
 }
 
-int main() {
-    const int64_t H = 2048, WO = 1792, DO = 257;
+int main(int argc, char** argv) {
+    // C3 window geometry by default; `c5`: configs[4]'s (4096 x 7936 x 257, 33 GB) -- the same store pattern at
+    // the bench's size (round 6: the C5 tile kernel runs at ~3.7 TB/s against ~4.2 at C3)
+    const bool c5 = argc > 1 && argv[1][0] == 'c' && argv[1][1] == '5';
+    const int64_t H = c5 ? 4096 : 2048, WO = c5 ? 7936 : 1792, DO = 257;
     const int64_t n = H * WO * DO;
     float* out;
     if (hipMalloc(&out, n * 4 + 4096) != hipSuccess) return 1;
@@ -129,6 +132,19 @@ int main() {
         printf("%-52s %8.4f ms  %7.1f GB/s\n", name, best, n * 4 / best / 1e6);
         fflush(stdout);
     };
+    if (c5) {  // the tile pattern (and the grid-stride ceiling) only
+        time("dword grid-stride nt", [&] { hipLaunchKernelGGL(k_dword<2>, dim3(8192), dim3(256), 0, 0, out, n); });
+        char nm5[96];
+        for (int TH : {64, 128, 32}) {
+            const int nTile = (int)((WO + 15) / 16), nBand = (int)((H + TH - 1) / TH);
+            snprintf(nm5, sizeof nm5, "C5 tile16 TH%d lds48K x4 nt bar", TH);
+            time(nm5, [&] {
+                hipLaunchKernelGGL((k_tile<true, 2, true, 1, 16>), dim3(nTile * nBand), dim3(256), 50000, 0, out, H, WO,
+                                   DO, TH, nTile);
+            });
+        }
+        return 0;
+    }
     time("dword grid-stride default", [&] { hipLaunchKernelGGL(k_dword<0>, dim3(8192), dim3(256), 0, 0, out, n); });
     time("dword grid-stride nt", [&] { hipLaunchKernelGGL(k_dword<2>, dim3(8192), dim3(256), 0, 0, out, n); });
     time("x4 grid-stride default", [&] { hipLaunchKernelGGL(k_x4<0>, dim3(8192), dim3(256), 0, 0, out, n / 4); });
