@@ -182,7 +182,14 @@ inline SweepGrid sweep_grid(const Geo& g, bool owned = false) {
     sg.S = owned ? sg.NL - margin : sg.NL;
     sg.nChunk = (int)(owned ? cdiv(ncol, (int64_t)sg.S) : cdiv(nd, (int64_t)sg.NL));
     sg.nTile = (int)cdiv(g.WO, TW);
-    sg.TH = 64;
+    // band height: the volume (owned) sweeps 128 rows -- half the K - 1 warm-up steps per output row of 64:
+    // C3 full 9.27-9.36 -> 9.11-9.12 ms, C2 full 1.13-1.16 -> 1.12-1.14 ms; the disparity partials keep 64
+    // (C2 full 1.77 -> 1.81 ms at 128), profiles/r06/j
+#ifdef CUSTMA_SWEEP_TH
+    sg.TH = CUSTMA_SWEEP_TH;  // (A/B builds)
+#else
+    sg.TH = owned ? 128 : 64;
+#endif
     // keep >= ~4 workgroups per CU on small problems
     while (sg.TH > 8 && (int64_t)sg.nTile * sg.nChunk * cdiv(g.HV(), sg.TH) < 2048) sg.TH /= 2;
     sg.nBand = (int)cdiv(g.HV(), sg.TH);

@@ -14,21 +14,19 @@ VARIANTS = {
     # backward loads two steps ahead (profiles/r04/a/bwd_depth_ab.txt)
     "bdp2": (["CUSTMA_BWD_DEPTH=2"], BWD),
     # knock-out (timing only, wrong results): k_bwd_coop without its volume loads -- the most an in-sweep
-    # recompute of the costs could save
+    # recompute of the costs could save (profiles/r06/a)
     "ko_novol": (["CUSTMA_KO_NOVOL"], BWD),
-    # the full-layout sweep with its round-5 dword volume stores (A/B against the 16-byte stores, round 6)
-    # the full-layout sweep's volume stores with the default cache policy instead of nt (round 6)
+    # without the chip-filling column segments of the backward sweep (profiles/r06/g, h)
+    "no_tail": (["CUSTMA_NO_TAIL"], BWD),
+    # the full-layout sweep's volume stores with the default cache policy instead of nt (profiles/r06/d)
     "sweep_plain": (["CUSTMA_SWEEP_AUX=0"], ["sweep_fwd.hip"]),
-    # without the tail-balanced column segments of the backward sweep
-    "no_tail": (["CUSTMA_NO_TAIL"], ["bwd_fused.hip"]),
-    # the full-layout sweep with its dword volume stores (A/B against the 16-byte stores, round 6)
+    # the full-layout sweep with its round-5 dword volume stores (profiles/r06/e)
     "sweep_dword": (["CUSTMA_SWEEP_NO_X4"], ["sweep_fwd.hip"]),
-    # the window tile forward / disparity with 32-row bands (the store pattern's best band, round 6)
+    # the full-layout sweep with 96 / 128-row bands (fewer K - 1 warm-up steps per output row)
+    "sweep_th96": (["CUSTMA_SWEEP_TH=96"], ["sweep_fwd.hip"]),
+    "sweep_th128": (["CUSTMA_SWEEP_TH=128"], ["sweep_fwd.hip"]),
+    # the window tile forward / disparity with 32-row bands (the store pattern's best band, profiles/r06/d)
     "th32": (["CUSTMA_WAVE_TH=32"], ["sweep_wave_d"]),
-    # statistics tile: 32 x 32 pixels, 4 rows per thread is the default (profiles/r03/stats)
-    "stats32x8": (["CUSTMA_STATS_TX=32", "CUSTMA_STATS_PR=8"], ["stats.hip"]),
-    "stats16x8": (["CUSTMA_STATS_TX=16", "CUSTMA_STATS_PR=8"], ["stats.hip"]),
-    "stats64x2": (["CUSTMA_STATS_TX=64", "CUSTMA_STATS_PR=2"], ["stats.hip"]),
 }
 # The round-1..3 ablation / knock-out builds (CUSTMA_ABL_*, rejected variants) were pruned from the
 # product sources in round 4; their measurements stay in DESIGN.md and profiles/.
