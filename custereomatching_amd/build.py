@@ -122,12 +122,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
 def build_variant(libdir: str, defines, only=None) -> str:
     """Ablation build (benchmarking only): the same library with extra -D switches into
     another directory; load it with CUSTMA_LIB=<path>.  `only`: the translation units the
-    switches affect, by source file or unit name (the rest link from the main build's objects)."""
+    switches affect, by source file or unit name (the rest link from the main build's objects
+    as they are).  The main library is never rebuilt here: an A/B's base is whatever was built
+    last, so a working-tree change under test cannot leak into it."""
     os.makedirs(libdir, exist_ok=True)
     extra = [d if d.startswith("-") else f"-D{d}" for d in defines]  # "-f..." flags pass through
     todo = [u for u in UNITS if only is None or u[1] in only or u[0] in only]
-    if only is not None:
-        build()
+    missing = [u[0] for u in UNITS if u not in todo and not os.path.exists(_obj(u))]
+    if missing:
+        raise RuntimeError(f"main-build objects missing for {missing}: run build() first")
     with cf.ThreadPoolExecutor(max_workers=max(1, min(len(todo), os.cpu_count() or 4))) as ex:
         done = dict(zip([u[0] for u in todo], ex.map(lambda u: _compile(u, extra, libdir), todo)))
     objs = [done.get(u[0], _obj(u)) for u in UNITS]

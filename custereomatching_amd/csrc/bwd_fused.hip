@@ -787,9 +787,10 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
     float* xs = xs_[wv];
     double* xp = xp_[wv];
     const double rk2 = 1.0 / (double)(K * K);
-    struct Ld { float g, x, y, mp, mc, c, p; double bc, bp; };
-    // loads of volume row h (zero outside the volume rows / columns: A_D = 0 there) and the raw
-    // images of row h + R (the product row that enters the patch sums at step h)
+    struct Ld { float g, x, y, mp, mc, c, p, pv, cv; double bc, bp; };
+    // loads of volume row h (zero outside the volume rows / columns: A_D = 0 there), the raw
+    // images of row h + R (the product row that enters the patch sums at step h) and the raw
+    // images of output row y = h - R (its T1 terms)
     auto load = [&](int h, Ld& b) {
         const bool hv = h >= hlo && h < hhi, hi = h >= 0 && h < Hi;
         const uint32_t vo = hv && vcol != OOB ? (uint32_t)(h - vb) * vstride + vcol : OOB;
@@ -807,6 +808,11 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
         const uint32_t eo = (uint32_t)(he * Wi) * 4u;
         b.c = ld_buf<float>(rP, ei && w >= 0 && w < Wi ? eo + (uint32_t)w * 4u + kC * pb4 : OOB);
         b.p = ld_buf<float>(rP, ei && w + Di >= 0 && w + Di < Wi ? eo + (uint32_t)(w + Di) * 4u + kP * pb4 : OOB);
+        const int yo = h - R;
+        const bool yi = own && yo >= 0 && yo < Hi;
+        const uint32_t yb = (uint32_t)(yo * Wi) * 4u;
+        b.pv = ld_buf<float>(rP, yi && w + Di >= 0 && w + Di < Wi ? yb + (uint32_t)(w + Di) * 4u + kP * pb4 : OOB);
+        b.cv = ld_buf<float>(rP, yi && w >= 0 && w < Wi ? yb + (uint32_t)w * 4u + kC * pb4 : OOB);
     };
     // horizontal box over the lanes x - R .. x + R of a product row (own lanes)
     auto hbox = [&](double v) {
@@ -840,11 +846,15 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
         ringP[(jj + 1) * 64 + lane] = pe;
         SP += pe;
     }
-    Ld cur, nxt;
-    load(hs, cur);
+    // Loads RP - 1 steps ahead in a ring of RP buffers indexed at compile time (the step loop unrolled RP
+    // times), so that no register copy at the loop's back edge waits for the newest loads, and every load
+    // of a step -- the strided gradient line included -- is issued RP - 1 steps before its use.  (Round 5:
+    // one step ahead through a copy, with the T1 image loads issued and used inside the step, so each step
+    // also waited for the next one's loads.)
+    constexpr int RP = 4;
+    Ld L[RP];
     int slot = 0;
-    for (int h = hs; h < he; ++h) {
-        load(h + 1, nxt);  // past the band: in range or masked, unused
+    auto step = [&](Ld& cur, int h) {
         {  // product row h + R enters, row h - R - 1 leaves (the forward's sliding fp64 sums)
             const double pe = hbox((double)cur.c * (double)cur.p);
             SP = (SP + pe) - ringP[slot * 64 + lane];
@@ -878,17 +888,26 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
             const int x = w;  // output column of an own lane
             if (own) {
                 const uint32_t ty = (uint32_t)((y - (int)a.ylo) * Wi * 4);
-                const uint32_t yi = (uint32_t)(y * Wi) * 4u;
                 // T1c at (y, x): p'(y, x + D) BoxA_D;  T1p at (y, x + D): c'(y, x) BoxA_D
                 const int xd = x + Di;
-                const float pv = ld_buf<float>(rP, xd >= 0 && xd < Wi ? yi + (uint32_t)xd * 4u + kP * pb4 : OOB);
-                const float cv = ld_buf<float>(rP, x >= 0 && x < Wi ? yi + (uint32_t)x * 4u + kC * pb4 : OOB);
-                if (x >= 0 && x < Wi) st_buf((pv - pb) * box, rT1, ty + (uint32_t)x * 4u);
-                if (xd >= 0 && xd < Wi) st_buf((cv - cb) * box, rT1, (uint32_t)(nywR * 4) + ty + (uint32_t)xd * 4u);
+                if (x >= 0 && x < Wi) st_buf((cur.pv - pb) * box, rT1, ty + (uint32_t)x * 4u);
+                if (xd >= 0 && xd < Wi) st_buf((cur.cv - cb) * box, rT1, (uint32_t)(nywR * 4) + ty + (uint32_t)xd * 4u);
             }
         }
-        cur = nxt;
+    };
+    Unroll<0, RP - 1>::run([&](auto ic) { load(hs + decltype(ic)::value, L[decltype(ic)::value]); });
+    int h = hs;
+    for (; h + RP <= he; h += RP) {
+        Unroll<0, RP>::run([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            load(h + i + RP - 1, L[(i + RP - 1) % RP]);  // past the band: in range or masked, unused
+            step(L[i], h + i);
+        });
     }
+    Unroll<0, RP - 1>::run([&](auto ic) {  // the last < RP steps (their loads were issued above)
+        constexpr int i = decltype(ic)::value;
+        if (h + i < he) step(L[i], h + i);
+    });
 }
 
 template <int K, bool WIN>

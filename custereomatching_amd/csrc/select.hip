@@ -303,6 +303,74 @@ __global__ __launch_bounds__(256) void k_disp_recheck(const T* __restrict__ cam,
     }
 }
 
+// k_disp_recheck with the queued pixel's k x k camera patch and its k x (DO + k - 1) projector strip staged in
+// LDS once (zero-padded, as float: tile_to_lds), so each of its DO diagonals runs the exact_cost chain from LDS
+// instead of 2 k^2 global loads (batched by 8 per patch row, each batch a round trip: the kernel was latency-
+// bound, ~40-60 us for ~150 pixels).  Same fp32 operations in the same order as exact_cost (bit-identical).
+template <typename T>
+__global__ __launch_bounds__(256) void k_disp_recheck_lds(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
+                                                          Stats sc, Stats sp, const int32_t* __restrict__ counter,
+                                                          const int64_t* __restrict__ queue, int64_t* __restrict__ idx,
+                                                          float* __restrict__ best, SoftOut so, int PX) {
+    extern __shared__ float rl[];
+    __shared__ float rv[4], r0[4], r1[4];
+    __shared__ int64_t ri[4];
+    const int k = g.k, r = k / 2;
+    float* tc = rl;          // [k][k]
+    float* tp = rl + k * k;  // [k][PX]: projector columns dmin - r .. dmin - r + PX - 1
+    const int n = *counter;
+    for (int64_t e = blockIdx.x; e < n; e += gridDim.x) {
+        const int64_t p = queue[e];
+        const int64_t h = g.h_lo + p / g.WO, w = p % g.WO;
+        const int64_t dmin = d_of_s(g, w, 0);
+        tile_to_lds<T>(cam, g.H, g.W, h - r, w - r, k, k, tc, k, (int)threadIdx.x, 256);
+        tile_to_lds<T>(proj, g.H, g.W, h - r, dmin - r, k, PX, tp, PX, (int)threadIdx.x, 256);
+        __syncthreads();
+        const float mc = sc.mean[h * g.W + w], qc = sc.sq[h * g.W + w];
+        float bv = -INFINITY, q0 = 0.f, q1 = 0.f;
+        int64_t bi = INT64_MAX;
+        for (int64_t s = threadIdx.x; s < g.DO; s += blockDim.x) {
+            const int64_t d = d_of_s(g, w, s);
+            if (!voxel_valid(g, w, d)) continue;
+            const float mp = sp.mean[h * g.W + d];
+            float acc = 0.f;
+            for (int i = 0; i < k; ++i) {
+                const float* cr = tc + i * k;
+                const float* pr = tp + i * PX + (int)(d - dmin);
+                for (int j = 0; j < k; ++j) acc = __builtin_fmaf(cr[j] - mc, pr[j] - mp, acc);
+            }
+            const float den = sqrtf(__builtin_fmaf(qc, sp.sq[h * g.W + d], kEps));
+            const float c = (acc + kEps) / den;
+            if (so.soft) soft_add(c, (float)s, bv, so.kb, q0, q1);
+            amax_merge(bv, bi, c, s);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ov = __shfl_xor(bv, off);
+            const int64_t oi = __shfl_xor(bi, off);
+            if (so.soft) {
+                const float o0 = __shfl_xor(q0, off), o1 = __shfl_xor(q1, off);
+                soft_merge(bv, ov, o0, o1, so.kb, q0, q1);
+            }
+            amax_merge(bv, bi, ov, oi);
+        }
+        const int wave = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) { rv[wave] = bv; ri[wave] = bi; r0[wave] = q0; r1[wave] = q1; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int q = 1; q < (int)(blockDim.x >> 6); ++q) {
+                if (so.soft) soft_merge(bv, rv[q], r0[q], r1[q], so.kb, q0, q1);
+                amax_merge(bv, bi, rv[q], ri[q]);
+            }
+            idx[p] = bi;
+            if (best) best[p] = bv;
+            if (so.mask) so.mask[p] = bv > so.threshold ? 1.f : 0.f;
+            if (so.soft) so.soft[p] = q1 / q0;
+        }
+        __syncthreads();  // (the next pixel's tiles overwrite this one's)
+    }
+}
+
 }  // namespace
 
 hipError_t launch_argmax(const float* vol, int64_t rows, int64_t n, int64_t* idx, float* best, hipStream_t s) {
@@ -391,7 +459,17 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
 #undef CUSTMA_K
         default: merge(std::integral_constant<int, 0>{});
     }
-    if (dtype == CUSTMA_F16) {
+    // the exact re-decision of the queued pixels: from LDS tiles while the projector strip fits 64 KiB
+    const int PX = (int)g.DO + g.k - 1;
+    const size_t rlds = sizeof(float) * (size_t)g.k * (size_t)(g.k + PX);
+    if (rlds <= 65536) {
+        if (dtype == CUSTMA_F16)
+            hipLaunchKernelGGL(k_disp_recheck_lds<__half>, dim3(2048), dim3(256), rlds, s, (const __half*)cam,
+                               (const __half*)proj, g, sc, sp, counter, queue, idx, best, so, PX);
+        else
+            hipLaunchKernelGGL(k_disp_recheck_lds<float>, dim3(2048), dim3(256), rlds, s, (const float*)cam,
+                               (const float*)proj, g, sc, sp, counter, queue, idx, best, so, PX);
+    } else if (dtype == CUSTMA_F16) {
         hipLaunchKernelGGL(k_disp_recheck<__half>, dim3(2048), dim3(256), 0, s, (const __half*)cam,
                            (const __half*)proj, g, sc, sp, counter, queue, idx, best, so);
     } else {

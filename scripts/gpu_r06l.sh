@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 6 (l): k_bwd_rem_rows with a 4-deep load ring (scripts/_abl/remring) against the main library:
-# (The variant was a working-tree change, measured and reverted: DESIGN.md §6 round-6 table describes it.)
+# (Run as r06o: the first run, r06l, compared two builds that both held the change -- build_variant relinked the main library then.)
 # backward parity subset on the variant, interleaved backward A/B (C5, C3, configs[2] window), kernel traces.
 set -o pipefail
 TAG=${1:-r06l}
