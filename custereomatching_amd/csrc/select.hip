@@ -197,9 +197,17 @@ __global__ __launch_bounds__(256) void k_disp_merge(const T* __restrict__ cam, c
 // in LDS, so a certified pixel's exact best cost reads its two k x k patches from LDS instead of
 // 2 k^2 global loads (the projector patch at a per-pixel disparity).  Same fp32 operations in the
 // same order as exact_cost (bit-identical).
-constexpr int kMTY = 4, kMTX = 64;
+// Tile rows (one wave each) x columns: 8 rows stage 18 / 8 projector-strip rows per pixel row at k = 11 where
+// 4 rows staged 14 / 4 -- the staging is the kernel's cost: C5 merge 0.85 -> 0.66 ms, C3 disparity 1.200 ->
+// 1.178 ms; 16 rows 0.78 ms (fewer resident workgroups), profiles/r06/q.  (Reading the patches as 8-byte pairs
+// from two staggered LDS copies doubled the kernel's time: twice the LDS, a third of the workgroups per CU,
+// profiles/r06/p.)
+#ifndef CUSTMA_MTY
+#define CUSTMA_MTY 8
+#endif
+constexpr int kMTY = CUSTMA_MTY, kMTX = 64;
 template <typename T, int KT>
-__global__ __launch_bounds__(256) void k_disp_merge_tile(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
+__global__ __launch_bounds__(64 * kMTY) void k_disp_merge_tile(const T* __restrict__ cam, const T* __restrict__ proj, Geo g,
                                                          Stats sc, Stats sp, DispPartial part, int nChunk, float tau,
                                                          int64_t* __restrict__ idx, float* __restrict__ best,
                                                          int32_t* __restrict__ counter, int64_t* __restrict__ queue,
@@ -210,8 +218,8 @@ __global__ __launch_bounds__(256) void k_disp_merge_tile(const T* __restrict__ c
     float* tc = tl;
     float* tp = tl + CY * CX;
     const int64_t x0 = (int64_t)(blockIdx.x % ntx) * kMTX, hy0 = g.h_lo + (int64_t)(blockIdx.x / ntx) * kMTY;
-    tile_to_lds<T>(cam, g.H, g.W, hy0 - R, x0 - R, CY, CX, tc, CX, (int)threadIdx.x, 256);
-    tile_to_lds<T>(proj, g.H, g.W, hy0 - R, x0 - R, CY, PX, tp, PX, (int)threadIdx.x, 256);
+    tile_to_lds<T>(cam, g.H, g.W, hy0 - R, x0 - R, CY, CX, tc, CX, (int)threadIdx.x, 64 * kMTY);
+    tile_to_lds<T>(proj, g.H, g.W, hy0 - R, x0 - R, CY, PX, tp, PX, (int)threadIdx.x, 64 * kMTY);
     __syncthreads();
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int64_t h = hy0 + ty, w = x0 + tx;
@@ -428,18 +436,18 @@ hipError_t launch_disparity(const void* cam, const void* proj, int dtype, const 
     // window layouts: the LDS-tiled merge while the projector strip fits
     const int ntx = (int)cdiv(g.WO, kMTX);
     const size_t mlds = sizeof(float) * (size_t)(kMTY + 2 * g.r) * (kMTX + 2 * g.r + (kMTX + g.D + 2 * g.r));
-    const bool mtile = g.layout == CUSTMA_LAYOUT_WINDOW && mlds <= 48 * 1024;
+    const bool mtile = g.layout == CUSTMA_LAYOUT_WINDOW && mlds <= 64 * 1024;
     const unsigned mtb = (unsigned)(ntx * cdiv(g.HV(), kMTY));
     auto merge = [&](auto kc) {
         constexpr int KT = decltype(kc)::value;
         if constexpr (KT > 0) {
             if (mtile) {
                 if (dtype == CUSTMA_F16)
-                    hipLaunchKernelGGL((k_disp_merge_tile<__half, KT>), dim3(mtb), dim3(256), mlds, s,
+                    hipLaunchKernelGGL((k_disp_merge_tile<__half, KT>), dim3(mtb), dim3(64 * kMTY), mlds, s,
                                        (const __half*)cam, (const __half*)proj, g, sc, sp, part, nChunk, tau, idx,
                                        best, counter, queue, so, ntx);
                 else
-                    hipLaunchKernelGGL((k_disp_merge_tile<float, KT>), dim3(mtb), dim3(256), mlds, s,
+                    hipLaunchKernelGGL((k_disp_merge_tile<float, KT>), dim3(mtb), dim3(64 * kMTY), mlds, s,
                                        (const float*)cam, (const float*)proj, g, sc, sp, part, nChunk, tau, idx,
                                        best, counter, queue, so, ntx);
                 return;
