@@ -11,8 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 BWD = ["bwd_fused.hip"]
 # name: (defines, translation units they affect)
 VARIANTS = {
-    # backward loads two steps ahead (profiles/r04/a/bwd_depth_ab.txt)
-    "bdp2": (["CUSTMA_BWD_DEPTH=2"], BWD),
+    # (CUSTMA_BWD_DEPTH=2, the backward's loads two steps ahead, profiles/r04/a/bwd_depth_ab.txt, no longer builds:
+    # its waits are runtime choices, which vmcnt_check.py cannot prove -- 7000 flagged reads in round 6)
     # knock-out (timing only, wrong results): k_bwd_coop without its volume loads -- the most an in-sweep
     # recompute of the costs could save (profiles/r06/a)
     "ko_novol": (["CUSTMA_KO_NOVOL"], BWD),
