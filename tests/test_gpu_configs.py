@@ -258,6 +258,24 @@ def test_large_and_even_kernel_sizes_through_autograd(gpu, k):
         assert np.array_equal(idx.cpu().numpy(), ridx)
 
 
+@pytest.mark.parametrize("layout", ["full", "window"])
+def test_disparity_recheck_both_forms(gpu, layout):
+    """k = 33 (no sliding instantiation: every pixel is re-decided with the exact arithmetic).  Full layout,
+    W = 600: the projector strip k x (W + k - 1) floats exceeds 64 KiB, so the re-decision runs the global-
+    load kernel (select.hip k_disp_recheck); window layout, D = 40: the LDS-tiled k_disp_recheck_lds.  Both
+    bit-identical to the oracle's argmax and best."""
+    H, W, D, k = 6, 600, 40, 33
+    cam, proj = make_pair(H, W, D, seed=733, kind="quantized")
+    c, p = _dev(cam, gpu), _dev(proj, gpu)
+    lay, Dl = (O.FULL, 0) if layout == "full" else (O.WINDOW, D)
+    ref = O.forward(cam, proj, k, layout=lay, D=Dl)
+    idx, best, nre = cm.stereo_disparity(c, p, D, k, layout, return_rechecked=True)
+    ridx, rbest = O.argmax(ref)
+    assert int(nre.item()) == H * ref.shape[1]  # every pixel re-decided
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    assert np.array_equal(best.cpu().numpy().view(np.uint32), np.asarray(rbest, np.float32).view(np.uint32))
+
+
 @pytest.mark.parametrize("k", [2, 4, 8, 16, 19, 22, 25, 28, 31])
 def test_sliding_kernel_sizes_through_autograd(gpu, k):
     """Even k (taps -k/2 .. k/2-1, stereo_matching_kernel.cu:44,60) and every k up to 31 on the sliding kernels:
