@@ -957,47 +957,65 @@ __global__ __launch_bounds__(64 * NWC) void k_bwd_coop(Geo g, BwdArgs a) {
 // Per (range class, column): the partial slots that hold the column (class 0 = camera
 // T1c / Am / B, which share one range; 1 = projector T1p; 2 = projector Ac / Bp).
 // cover layout: [3][W] counts, then [3][W][S] slot indices (uint16).
-// cover_column counts every (chunk, segment) whose written range holds column x and stores the
-// first S slot indices into `list` (when given).  plan_bwd's S bounds the count by construction
+// k_bwd_cover counts every (chunk, segment) whose written range holds column x and lists the first S
+// slot indices, in chunk order, then segment order.  plan_bwd's S bounds the count by construction
 // (2 x the max chunk overlap, <= 2 segments per chunk); the device marks an over-full column with
 // count -1, which k_bwd_gather turns into NaN gradients -- never a silently dropped slot.
-__host__ __device__ inline int cover_column(const Geo& g, int64_t dlo, int nChunk, int S, int Sj, int64_t x, int cls,
-                                            unsigned short* list) {
+// The slots of chunk j whose written range of class cls holds column x, in segment order (at most 2,
+// adjacent segments; more are counted but not stored): their count, the first two into e.
+__host__ __device__ inline int chunk_cover(const Geo& g, int64_t dlo, int Sj, int64_t x, int cls, int j,
+                                           unsigned short* e) {
     const int t = cls == 0 ? 0 : cls == 1 ? 3 : 4;
+    const ChunkGeo c = chunk_geo(g, dlo, j);
+    int64_t lo, hi;
+    type_range(c, taps_of(g), t, &lo, &hi);
+    if (x < lo || x >= hi) return 0;
+    const int ns = chunk_nseg(c, taps_of(g));
+    const Taps tp = taps_of(g);
+    const int64_t rel = x - (c.wlo - tp.r0) - (cls ? c.d0 : 0);
+    // segments whose written range can hold x: relative to segment s's own first column
+    // s seg, every range lies in [-k, seg + r0 + 63) (seg_range); checked exactly below
+    auto fdiv = [](int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
+    const int s_lo = (int)fdiv(rel - c.seg - tp.r0 - NLB, c.seg);
+    const int s_hi = (int)fdiv(rel + g.k, c.seg);
     int n = 0;
-    for (int j = 0; j < nChunk; ++j) {
-        const ChunkGeo c = chunk_geo(g, dlo, j);
-        int64_t lo, hi;
-        type_range(c, taps_of(g), t, &lo, &hi);
-        if (x < lo || x >= hi) continue;
-        const int ns = chunk_nseg(c, taps_of(g));
-        // the segment(s) of chunk j whose written range holds column x (<= 2, adjacent)
-        const Taps tp = taps_of(g);
-        const int64_t rel = x - (c.wlo - tp.r0) - (cls ? c.d0 : 0);
-        // segments whose written range can hold x: relative to segment s's own first column
-        // s seg, every range lies in [-k, seg + r0 + 63) (seg_range); checked exactly below
-        auto fdiv = [](int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
-        const int s_lo = (int)fdiv(rel - c.seg - tp.r0 - NLB, c.seg);
-        const int s_hi = (int)fdiv(rel + g.k, c.seg);
-        for (int sg = s_lo < 0 ? 0 : s_lo; sg <= s_hi; ++sg) {
-            if (sg < 0 || sg >= ns) continue;
-            seg_range(c, tp, sg, t, &lo, &hi);
-            if (x >= lo && x < hi) {
-                if (list && n < S) list[n] = (unsigned short)(2 * (j % Sj) + (sg & 1));
-                ++n;
-            }
+    for (int sg = s_lo < 0 ? 0 : s_lo; sg <= s_hi; ++sg) {
+        if (sg < 0 || sg >= ns) continue;
+        seg_range(c, tp, sg, t, &lo, &hi);
+        if (x >= lo && x < hi) {
+            if (n < 2) e[n] = (unsigned short)(2 * (j % Sj) + (sg & 1));
+            ++n;
         }
     }
     return n;
 }
+// One wave per (range class, column), lane = chunk (blocks of 64 chunks): each lane finds its chunk's slots
+// and a ballot prefix places them after the lower chunks', so the list is in chunk order, then segment
+// order -- the order k_bwd_gather sums in.  (Round 5: one thread per column ran the serial loop over
+// every chunk and class, W threads in all: ~70-90 us at C2 full, where W / 256 = 4 workgroups.)
 __global__ __launch_bounds__(256) void k_bwd_cover(Geo g, int64_t dlo, int nChunk, int S, int Sj, int* cover) {
-    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= g.W) return;
-    unsigned short* list = (unsigned short*)(cover + 3 * g.W);
-    for (int cls = 0; cls < 3; ++cls) {
-        const int n = cover_column(g, dlo, nChunk, S, Sj, x, cls, list + ((size_t)cls * g.W + x) * S);
-        cover[cls * g.W + x] = n <= S ? n : -1;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = (int)(threadIdx.x & 63);
+    if (wid >= 3 * g.W) return;  // wave-uniform
+    const int cls = (int)(wid / g.W);
+    const int64_t x = wid - (int64_t)cls * g.W;
+    unsigned short* list = (unsigned short*)(cover + 3 * g.W) + ((size_t)cls * g.W + x) * S;
+    const uint64_t below = (1ull << lane) - 1;
+    int n = 0;  // slots listed by the lower chunks (wave-uniform)
+    for (int j0 = 0; j0 < nChunk; j0 += 64) {
+        const int j = j0 + lane;
+        unsigned short e[2] = {0, 0};
+        const int c = j < nChunk ? chunk_cover(g, dlo, Sj, x, cls, j, e) : 0;
+        const uint64_t b1 = __ballot(c >= 1), b2 = __ballot(c >= 2);
+        const int pos = n + __popcll(b1 & below) + __popcll(b2 & below);
+        if (c >= 1 && pos < S) list[pos] = e[0];
+        if (c >= 2 && pos + 1 < S) list[pos + 1] = e[1];
+        n += __popcll(b1) + __popcll(b2);
+        // more than two segments of one chunk never hold a column (adjacent segments only); if one did,
+        // the column reads as over-full (NaN gradients in k_bwd_gather), never as a dropped slot
+        if (__ballot(c >= 3)) n = S + 1;
     }
+    if (lane == 0) cover[cls * g.W + x] = n <= S ? n : -1;
 }
 
 // Sum of the partial slots of type 3 side + q at pixel p = (y, x) (fp64, even / odd slots in two
@@ -1541,7 +1559,7 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     const int64_t n = g.H * g.W;
     hipLaunchKernelGGL(k_img_blocksum<T>, dim3(kSumBlocks, 2), dim3(256), 0, s, cam, proj, n, bsum);
     hipLaunchKernelGGL(k_img_shift, dim3(1), dim3(256), 0, s, bsum, kSumBlocks, n, shift);
-    hipLaunchKernelGGL(k_bwd_cover, dim3((unsigned)cdiv(g.W, 256)), dim3(256), 0, s, g, p.dlo, p.nChunk, p.S, p.Sj,
+    hipLaunchKernelGGL(k_bwd_cover, dim3((unsigned)cdiv(3 * g.W * 64, 256)), dim3(256), 0, s, g, p.dlo, p.nChunk, p.S, p.Sj,
                        cover);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
