@@ -747,10 +747,14 @@ __device__ __forceinline__ void bwd_coop_body(const Geo& g, const BwdArgs& a, in
 // the forward's own fp64 arithmetic for fp32), cost = (float)(E + eps) rsq(X Y + eps) with the
 // same fp32 moments as A_D.  A wave owns the 64 - 2R middle columns of its 64 (the outer R on each
 // side only feed the horizontal boxes); one wave per (column tile, row band).
-constexpr int kRemRB = 64;  // output rows per row band
+constexpr int kRemRB = 64;  // output rows per row band (at most; run_bwd halves it on small grids)
+#ifndef CUSTMA_REM_WAVES
+#define CUSTMA_REM_WAVES 4096
+#endif
+constexpr int kRemWaves = CUSTMA_REM_WAVES;  // waves k_bwd_rem_rows aims for (A/B builds set CUSTMA_REM_WAVES)
 
 template <int K>
-__global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntile) {
+__global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntile, int rb) {
     constexpr int R = K / 2, OWN = 64 - 2 * R;
     __shared__ float xs_[4][64];
     __shared__ double xp_[4][64];
@@ -760,9 +764,9 @@ __global__ __launch_bounds__(256) void k_bwd_rem_rows(Geo g, BwdArgs a, int ntil
     const int64_t unit = (int64_t)blockIdx.x * 4 + wv;
     const int tile = (int)(unit % ntile);
     const int64_t band = unit / ntile;
-    const int64_t y0 = a.ylo + band * kRemRB;
+    const int64_t y0 = a.ylo + band * rb;
     if (y0 >= a.yhi) return;
-    const int64_t y1 = min(a.yhi, y0 + kRemRB);
+    const int64_t y1 = min(a.yhi, y0 + rb);
     const int Wi = (int)g.W, WOi = (int)g.WO, Di = (int)g.D, hlo = (int)g.h_lo, hhi = (int)g.h_hi, Hi = (int)g.H;
     const int x0 = -R + tile * OWN;          // first output column of this wave
     const int w = x0 - R + lane;             // this lane's camera column (voxel column)
@@ -1587,7 +1591,12 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
     const unsigned blocks = (unsigned)(8 * (int64_t)nU * p.nsegMax * cdiv(p.nRG, 8));
     // k_bwd_rem_rows: one wave per (column tile of 64 - 2r owned columns over [-r, WO + r), row band)
     const int rem_tiles = (int)cdiv(g.WO + 2 * g.r, 64 - 2 * g.r);
-    const int64_t rem_units = (int64_t)rem_tiles * cdiv(p.yhi - p.ylo, kRemRB);
+    // Row bands of kRemRB rows, halved while the grid has fewer than kRemWaves waves: a wave walks its band
+    // row by row with one strided gradient line per step, so a small grid (C3: 1088 waves of 64 rows, about
+    // one per SIMD) is latency-bound; shorter bands walk more warm-up rows (K - 1 per band) in parallel.
+    int rem_rb = kRemRB;
+    while (rem_rb > 8 && (int64_t)rem_tiles * cdiv(p.yhi - p.ylo, rem_rb) < kRemWaves) rem_rb /= 2;
+    const int64_t rem_units = (int64_t)rem_tiles * cdiv(p.yhi - p.ylo, rem_rb);
     if (units > 0) {
         const bool win = win_path_ok(g);
         prof_begin(PROF_BWD, s);
@@ -1610,7 +1619,8 @@ hipError_t run_bwd(const float* grad, const float* vol, const T* cam, const T* p
         switch (g.k) {
 #define CUSTMA_K(KK)                                                                                             \
     case KK:                                                                                                            \
-        hipLaunchKernelGGL((k_bwd_rem_rows<KK>), dim3((unsigned)cdiv(rem_units, 4)), dim3(256), 0, s, g, a, rem_tiles); \
+        hipLaunchKernelGGL((k_bwd_rem_rows<KK>), dim3((unsigned)cdiv(rem_units, 4)), dim3(256), 0, s, g, a, rem_tiles, \
+                           rem_rb);                                                                                     \
         break;
             CUSTMA_SWEEP_KS(CUSTMA_K)
 #undef CUSTMA_K
