@@ -230,6 +230,27 @@ def test_config4_window_fp16_one_gpu(gpu):
     assert torch.isfinite(gc).all() and torch.isfinite(gp).all()
 
 
+def test_backward_rank_band_full_width(gpu):
+    """The N = 8 rank band of configs[4] (512 rows + 2 x 5 halo rows of 4096 x 8192 fp16, D = 256, k = 11): a
+    backward grid with a partial last round, where run_bwd may re-segment the columns (bwd_fused.hip
+    tail_seg_min); checked on haloed oracle tiles at both ends of the row and in the middle."""
+    H, W, k, D = 522, 8192, 11, 256
+    cam, proj = make_pair(H, W, D, seed=111)
+    c, p = _dev(cam, gpu, torch.float16), _dev(proj, gpu, torch.float16)
+    c32, p32 = _f16(cam), _f16(proj)
+    fa = cm.cost_volume_forward(c, p, D, k, "window", "fast")
+    gen = torch.Generator(device=gpu).manual_seed(112)
+    g = torch.randn(fa.shape, generator=gen, device=gpu)
+    gc, gp = cm.cost_volume_backward(g, c, p, k, "window", D, projector_grad=True, cost_volume=fa)
+    for h0 in (0, 258, 516):
+        for c0 in (0, 3712, W - 768):
+            h1 = min(H, h0 + 6)
+            rc, rp, (xc0, xc1), (xp0, xp1) = _tile_backward(g, c32, p32, k, D, h0, h1, c0, 768)
+            assert _rel(gc[h0:h1, xc0:xc1].cpu().numpy(), rc) <= 1e-5, (h0, c0)
+            assert _rel(gp[h0:h1, xp0:xp1].cpu().numpy(), rp) <= 1e-5, (h0, c0)
+    assert torch.isfinite(gc).all() and torch.isfinite(gp).all()
+
+
 
 # ---------------- kernel sizes beyond the fused instantiations (generic paths) ----------------
 
