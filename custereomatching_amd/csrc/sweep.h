@@ -202,7 +202,7 @@ struct WaveGrid {
     int nChunk, nTile, nBand, TH;
     bool rem;  // window, (D+1) % 64 == 1: the last chunk's waves add diagonal D
 };
-WaveGrid wave_grid(const Geo& g);
+WaveGrid wave_grid(const Geo& g, bool disparity = false);
 hipError_t launch_fwd_lds(const void* cam, const void* proj, int dtype, const Geo& g, Stats sc, Stats sp,
                           float* out, hipStream_t s);
 

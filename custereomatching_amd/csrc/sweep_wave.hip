@@ -707,7 +707,7 @@ hipError_t launch_k(const T* cam, const T* proj, const Geo& g, Stats sc, Stats s
 // Fused disparity through the tile kernel (window layout, D + 1 <= 257): one partial per pixel.
 template <int K, typename T>
 hipError_t launch_amx(const T* cam, const T* proj, const Geo& g, Stats sc, Stats sp, DispPartial part, hipStream_t s) {
-    const WaveGrid wg = wave_grid(g);
+    const WaveGrid wg = wave_grid(g, /*disparity=*/true);
     const int64_t blocks = (int64_t)wg.nBand * wg.nTile;
     // (no camera preload here: it measured slower, C5 9.69 -> 9.99 ms, C3 1.15 -> 1.18 ms)
     const size_t lds = (size_t)wg.nChunk * kWaveLds + 2 * TW * (size_t)kAmxPitch * 4;
@@ -748,7 +748,7 @@ template hipError_t sw_amx<CUSTMA_SW_K>(const void*, const void*, int, const Geo
 #else  // CUSTMA_SW_DISPATCH
 
 
-WaveGrid wave_grid(const Geo& g) {
+WaveGrid wave_grid(const Geo& g, bool disparity) {
     WaveGrid wg;
     const int64_t nd = g.layout == CUSTMA_LAYOUT_WINDOW ? (int64_t)g.D + 1 : g.W + TW - 1;
     wg.nChunk = (int)cdiv(nd, 64);
@@ -766,6 +766,11 @@ WaveGrid wave_grid(const Geo& g) {
     // (a tail-balanced band height -- the one with the fewest rounds x (TH + k - 1) steps on 3 workgroups per
     // CU, TH = 61 at C3 -- measured no faster for the volume and 1.7 % slower for the disparity, round 6:
     // profiles/r06/g)
+    // The fused disparity on large grids (>= 16 rounds of 128-row bands on 3 workgroups per CU of a 256-CU
+    // part: configs[4]'s whole image) takes 128-row bands, half the K - 1 warm-up steps per output row: C5
+    // disparity 9.69 -> 9.50 ms; C3 unchanged, a C5 rank band 1.45 -> 1.61 ms and every volume forward slower
+    // at 128 (profiles/r06/ab), so those keep 64.
+    if (disparity && wg.TH == 64 && (int64_t)wg.nTile * cdiv(g.HV(), 128) >= 16 * 3 * 256) wg.TH = 128;
     wg.nBand = (int)cdiv(g.HV(), wg.TH);
     return wg;
 }
